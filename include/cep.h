@@ -1,0 +1,198 @@
+/* cep.h — C ABI of libcep.so, the MI355X-native CEP matcher.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference runs one
+ * NFA inside a Kafka Streams Processor and is driven record by record:
+ *
+ *   new CEPProcessor<>(pattern[, inMemory])            CEPProcessor.java:71-84
+ *   CEPProcessor.init(ProcessorContext)                CEPProcessor.java:88-108
+ *   CEPProcessor.process(K, V) -> context.forward(null, Sequence) per match
+ *                                                      CEPProcessor.java:155-163
+ *   NFA.matchPattern(K, V, long) -> List<Sequence>     nfa/NFA.java:94-109
+ *   StatesFactory.make(Pattern) -> List<Stage>         pattern/StatesFactory.java:41-63
+ *
+ * Here a query (the serialised Pattern chain with its where/fold lambdas lowered to a
+ * typed IR, see "Query IR" below) is compiled once (cep_query_compile ~ StatesFactory.make),
+ * a session holds the per-key NFA state on one GPU (~ CEPProcessor.init + NFA), and records
+ * arrive as key-partitioned column batches (cep_push_batch ~ a run of process() calls);
+ * matches come back as flat arrays (cep_poll_matches ~ the forwarded Sequences).
+ *
+ * Semantics: one reference NFA per key ("key" = independent stream), results
+ * bit-exact with the reference on the same inputs, including its exceptions, which are
+ * reported per key (cep_key_errors) instead of killing the stream thread.
+ *
+ * Threading: a session is used from one thread at a time (the reference's Processor is
+ * single-threaded too); sessions are independent.  All functions return CEP_OK (0) or a
+ * negative CEP_E_* status; cep_last_error() has the message (thread-local).
+ */
+#ifndef CEP_H_
+#define CEP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CEP_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define CEP_OK 0
+#define CEP_E_INVALID (-1)   /* bad argument */
+#define CEP_E_HIP (-2)       /* HIP runtime error */
+#define CEP_E_NOMEM (-3)     /* device allocation failed */
+#define CEP_E_COMPILE (-4)   /* query compile error (see cep_query_compile) */
+#define CEP_E_STATE (-5)     /* call out of order */
+
+/* ---- per-key error codes: the reference exception that would escape process() ---- */
+#define CEP_KEY_OK 0
+#define CEP_KEY_NPE 1            /* NullPointerException (null fold unboxing, H2/H3 walks, ...) */
+#define CEP_KEY_ILLEGAL_STATE 2  /* IllegalStateException "Cannot find predecessor event"
+                                    (nfa/buffer/impl/KVSharedVersionedBuffer.java:86-89) */
+#define CEP_KEY_ARITHMETIC 3     /* ArithmeticException (integer / or % by zero in a lambda) */
+#define CEP_KEY_CAPACITY 16      /* this build only: a per-key limit (live runs, Dewey width,
+                                    buffer pools) was exceeded; never silent */
+
+/* ---- compile-time errors, returned in cep_query_info.compile_error ---- */
+#define CEP_COMPILE_NPE 1              /* pattern ending in a Kleene/optional stage (StatesFactory:102) */
+#define CEP_COMPILE_ILLEGAL_ARGUMENT 4 /* a pattern without where() (Stage.java:159) */
+
+/* ---- Query IR (produced by kafkastreams-cep_amd/pattern.py Pattern.to_ir) ----
+ * little-endian; str = u16 length + UTF-8 bytes
+ *   "CEPQ" u32 version(=1)
+ *   u16 n_fields  { u8 type; str name }      event columns (type: 1=int 2=long 3=double)
+ *   u16 n_states  { u8 type; str name }      fold states (boxed Integer/Long/Double)
+ *   u16 n_names   { str name }               distinct stage names (output stage ids index this)
+ *   u16 n_patterns, first to last:
+ *       u16 name; u8 cardinality (0 ONE,1 OPTIONAL,2 ZERO_OR_MORE,3 ONE_OR_MORE);
+ *       u8 strategy (0 STRICT,1 SKIP_TIL_NEXT,2 SKIP_TIL_ANY); u8 has_window; i64 window_ms;
+ *       u8 has_pred; [expr]; u16 n_aggs { u16 state; expr }
+ *   expr (prefix): u8 op, then
+ *     01 CONST_I32 i32 | 02 CONST_I64 i64 | 03 CONST_F64 f64 | 04 CONST_BOOL u8
+ *     05 FIELD u16 | 06 TS | 07 STATE_GET u16 (nullable) | 08 STATE_GET_OR u16 expr(default)
+ *     09 CURR (nullable; fold only)
+ *     10 ADD 11 SUB 12 MUL 13 DIV 14 REM: u8 type, expr, expr   (Java int/long/double rules)
+ *     15 NEG u8 type expr | 18 CAST u8 from u8 to expr
+ *     20 LT 21 LE 22 GT 23 GE 24 EQ 25 NE: u8 operand type, expr, expr
+ *     30 AND expr expr | 31 OR expr expr | 32 NOT expr   (short-circuit, left first)
+ *   Operands are already promoted (explicit CASTs); a nullable operand is unboxed where used.
+ */
+
+typedef struct cep_query cep_query;
+typedef struct cep_session cep_session;
+
+typedef struct {
+  uint32_t n_patterns;
+  uint32_t n_stages;      /* compiled stages incl. $final and ONE_OR_MORE wrappers */
+  uint32_t n_names;       /* stage-name ids 0..n_names-1 used in match output */
+  uint32_t n_fields;
+  uint32_t n_states;
+  uint32_t kind;          /* CEP_KIND_* : which kernel runs this query */
+  uint32_t arity;         /* CEP_KIND_STENCIL: events per match (else 0) */
+  int32_t compile_error;  /* 0, CEP_COMPILE_NPE or CEP_COMPILE_ILLEGAL_ARGUMENT */
+} cep_query_info;
+
+#define CEP_KIND_NFA 0      /* general NFA kernel (runs, shared versioned buffer, folds) */
+#define CEP_KIND_STENCIL 1  /* proven specialisation: all stages ONE + strict, total
+                               state-free predicates, distinct names */
+
+/* Compile a serialised Pattern chain.  On a reference compile-time exception the call
+ * still succeeds and info.compile_error says which (sessions then refuse the query). */
+int cep_query_compile(const uint8_t* ir, size_t n, cep_query** out);
+int cep_query_info_get(const cep_query* q, cep_query_info* info);
+/* stage name of id `name_id` (UTF-8, NUL-terminated, owned by the query) */
+const char* cep_query_stage_name(const cep_query* q, uint32_t name_id);
+void cep_query_destroy(cep_query* q);
+
+typedef struct {
+  int device;             /* HIP device ordinal */
+  int force_nfa;          /* 1: run CEP_KIND_STENCIL queries on the general NFA kernel */
+  uint32_t max_runs;      /* live runs per key (0 = default 32); retried x8 on overflow */
+  double pool_factor;     /* buffer pool size per event of the batch (0 = default) */
+} cep_opts;
+
+int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts,
+                       cep_session** out);
+void cep_session_destroy(cep_session* s);
+
+#define CEP_MEM_HOST 0
+#define CEP_MEM_DEVICE 1
+
+/* A key-partitioned (CSR) column batch: events of key k are positions
+ * key_off[k] .. key_off[k+1]-1, in arrival order.  cols[f] holds n_events values of the
+ * IR field type f.  ts may be NULL (timestamps are not read by WITHIN in the reference:
+ * its windows never prune).  Buffers are borrowed for the call only. */
+typedef struct {
+  uint64_t n_keys;
+  uint64_t n_events;
+  const uint64_t* key_off;  /* [n_keys + 1] */
+  const void* const* cols;  /* [n_fields] */
+  const int64_t* ts;        /* [n_events] or NULL */
+  int memory;               /* CEP_MEM_HOST or CEP_MEM_DEVICE */
+} cep_batch;
+
+/* Runs every query of the session over the batch.  Each batch starts every key from the
+ * NFA's initial state (one batch = one stream segment per key).  Asynchronous on the
+ * session's stream; cep_sync / cep_poll_matches wait for it. */
+int cep_push_batch(cep_session* s, const cep_batch* b);
+int cep_sync(cep_session* s);
+
+/* Matches of query `query` for the last batch, ordered by key then emission order (the
+ * order the reference forwards them per key).  A match is the Sequence walk of
+ * KVSharedVersionedBuffer.remove (nfa/buffer/impl/KVSharedVersionedBuffer.java:143-171):
+ * pairs (stage name id, event) from the final event back to the first; events are given
+ * as sequence numbers within the key (CSR position = key_off[key] + seq).
+ * CEP_KIND_STENCIL queries return fixed-arity matches: pair_off/pair_stage are NULL,
+ * match i owns pairs [i*arity, (i+1)*arity) with stage ids arity_stage[0..arity-1].
+ * Arrays live in `memory` space and stay valid until the next push/poll/destroy. */
+typedef struct {
+  uint64_t n_matches;
+  uint64_t n_pairs;
+  uint32_t arity;                /* 0: variable-length (use pair_off) */
+  const uint16_t* arity_stage;   /* host memory, [arity] (fixed-arity only) */
+  const uint32_t* key;           /* [n_matches] */
+  const uint32_t* emit_seq;      /* [n_matches] event whose arrival completed the match */
+  const uint64_t* pair_off;      /* [n_matches + 1] or NULL */
+  const uint32_t* pair_seq;      /* [n_pairs] */
+  const uint16_t* pair_stage;    /* [n_pairs] or NULL */
+  int memory;
+} cep_matches;
+
+int cep_poll_matches(cep_session* s, int query, int memory, cep_matches* out);
+
+/* Per-key reference exceptions of the last batch: code[k] (CEP_KEY_*) and the sequence
+ * number of the event whose processing threw (matches of earlier events are kept). */
+int cep_key_errors(cep_session* s, int query, int32_t* code, uint32_t* seq, uint64_t n_keys);
+
+/* Order-independent match checksum (Σ over matches of a 64-bit hash of key, emit and the
+ * pair list) and count, computed on the device: what ranks all-gather over RCCL. */
+int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* checksum);
+
+/* Largest timestamp of the last batch (INT64_MIN without ts): the rank-local watermark
+ * that multi-GPU runs reduce with min. */
+int cep_watermark(cep_session* s, int64_t* out);
+
+/* Device time of the last batch's matching kernels, per query, from HIP events recorded
+ * on the session stream (ms), and the launch count. */
+int cep_last_timing(cep_session* s, int query, double* kernel_ms, uint32_t* launches);
+
+const char* cep_last_error(void);
+int cep_alloc_pinned(size_t bytes, void** out);
+int cep_free_pinned(void* p);
+int cep_device_alloc(int device, size_t bytes, void** out);
+int cep_device_free(void* p);
+int cep_memcpy(void* dst, const void* src, size_t bytes, int dst_memory, int src_memory);
+
+/* ---- synthetic workloads (bench / tests): kafkastreams-cep_amd/workloads.py, on device ----
+ * kind 0 = "abc" (one int column v = h % 16), 1 = "stock" (int price random walk, int volume).
+ * Fills device buffers: key_off [n_keys+1] (u64), cols[0..] (int32, n_events each).
+ * cep_synth_count returns n_events for sizing. */
+int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
+                    uint32_t mean_events, uint64_t* n_events);
+int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
+                       uint32_t mean_events, uint64_t* key_off_dev, int32_t* const* cols_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CEP_H_ */

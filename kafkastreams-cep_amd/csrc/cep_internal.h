@@ -1,0 +1,51 @@
+// cep_internal.h — host-side structures of libcep.so (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/cep.h"
+#include "cep_layout.h"
+
+struct cep_query {
+  cep_query_info info{};
+  cep::DevQuery dev{};
+  std::vector<uint32_t> code;
+  std::vector<std::string> names, fieldNames, stateNames;
+  // CEP_KIND_STENCIL
+  std::vector<uint16_t> arityStage;   // walk order stage names
+  std::vector<uint16_t> stencilProg;  // predicate program per pattern (first..last)
+  bool stencilRange = false;          // every predicate is a conjunction of int ranges
+  int rangeCols[2] = {0, 0};
+  int nRangeCols = 0;
+  int64_t rangeLo[8][2]{}, rangeHi[8][2]{};
+};
+
+namespace cep {
+
+void compile_query(const uint8_t* ir, size_t n, cep_query* q);
+
+struct NfaArgs;
+struct StencilArgs;
+struct KeyState;
+
+hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
+size_t rec_size(int F);
+hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
+                          uint64_t* totals, hipStream_t st);
+hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
+                          const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
+                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals,
+                          unsigned long long* digest, hipStream_t st);
+hipError_t launch_tile_first_key(const uint64_t* key_off, uint64_t n_keys, uint32_t* tile_key, uint64_t n_events,
+                                 hipStream_t st);
+hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
+uint64_t stencil_tiles(uint64_t n_events);
+hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, const uint64_t* key_off,
+                        int32_t* c0, int32_t* c1, hipStream_t st);
+hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
+uint64_t synth_hash_host(uint64_t seed, uint64_t key, uint64_t j);
+
+}  // namespace cep

@@ -1,0 +1,133 @@
+// cep_layout.h — device data layout shared by the host compiler and the HIP kernels.
+//
+// One reference NFA per key.  The reference keeps, per NFA (nfa/NFA.java:50-56):
+//   a FIFO of ComputationStage run records      -> a per-key ring of Rec in HBM
+//   KVSharedVersionedBuffer nodes + predecessor  -> pooled Node / Pred entries in HBM,
+//     lists, keyed (stage name, type, offset)       found through a per-event node chain
+//   ValueStore fold values keyed (state, run seq) -> inline fold registers in Rec
+//   DeweyVersion int[]                           -> run-length encoded (value, count) pairs
+// Layout rationale and the proofs behind the inline folds / node chains: DESIGN.md §3.
+#pragma once
+#include <stdint.h>
+
+#define CEP_NONE 0xFFFFFFFFu
+
+namespace cep {
+
+constexpr int kMaxStages = 32;     // compiled stages per query (2m+1 for m patterns)
+constexpr int kMaxStageKeys = 32;  // distinct (name, type) pairs
+constexpr int kMaxFields = 16;
+constexpr int kMaxStates = 8;      // fold state names per query (MAXF)
+constexpr int kMaxAggs = 8;        // folds per pattern
+constexpr int kMaxStack = 16;      // interpreter stack depth
+constexpr int kDeweyPairs = 6;     // RLE pairs per Dewey version (overflow -> CEP_KEY_CAPACITY)
+
+enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
+enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3 };
+enum KeyErr : int32_t { KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16 };
+
+constexpr uint16_t kProgTrue = 0xFFFF;
+
+struct DevEdge {
+  uint8_t op;
+  uint8_t target;  // stage index (0xFF: none, IGNORE)
+  uint16_t prog;   // predicate program offset in code[], kProgTrue = constant true
+};
+
+struct DevStage {
+  uint8_t sk;      // interned (name, type) — Stage.equals / StateKey identity
+  uint8_t type;    // StateType
+  uint8_t n_edges;
+  uint8_t n_aggs;
+  DevEdge e[3];    // edge order [BEGIN|TAKE, IGNORE?, PROCEED?] (StatesFactory.java:80-107)
+  uint16_t agg_state[kMaxAggs];
+  uint16_t agg_prog[kMaxAggs];
+};
+
+struct DevQuery {
+  uint32_t n_stages, n_sk, n_states, n_fields;
+  uint32_t begin_stage;  // StatesFactory.make's last element (the only BEGIN stage)
+  uint32_t code_len;     // words
+  uint8_t sk_type[kMaxStageKeys];
+  uint16_t sk_name[kMaxStageKeys];
+  uint8_t field_type[kMaxFields];  // 1 int, 2 long, 3 double
+  uint8_t state_type[kMaxStates];
+  DevStage st[kMaxStages];
+};
+
+// ---- Dewey version, run-length encoded: digits = v[0] x c[0], v[1] x c[1], ...
+struct Dewey {
+  uint32_t n;    // pairs in use
+  uint32_t len;  // number of digits (DeweyVersion.length())
+  int32_t v[kDeweyPairs];
+  uint32_t c[kDeweyPairs];
+};
+
+// ---- run record (ComputationStage, nfa/ComputationStage.java:29-157)
+// stage word: [7:0] stage index (real) or epsilon target; [15:8] stage key; bit16 epsilon;
+// bit17 branching flag.  Epsilon stages (Stage.newEpsilonState) are (source key, target).
+constexpr uint32_t kRecEps = 1u << 16;
+constexpr uint32_t kRecBranch = 1u << 17;
+constexpr uint32_t kRecFinal = 1u << 18;  // transient: forwarding to $final (in-step only)
+
+template <int F>
+struct Rec {
+  uint32_t stage;
+  uint32_t event;     // sequence number of the run's last event within the key, CEP_NONE = null
+  uint32_t ev_first;  // head of the node chain of `event` (CEP_NONE: none / pending)
+  uint32_t nullmask;  // bit s: fold state s is null
+  Dewey ver;
+  int64_t fold[F];
+};
+
+// ---- buffer node (TimedKeyValue + its StackEventKey, nfa/buffer/impl/TimedKeyValue.java)
+struct Node {
+  uint32_t event;      // sequence number within key
+  int32_t refs;        // TimedKeyValue.refs
+  uint32_t head, tail; // predecessor list (Pred indices), insertion order
+  uint32_t same_next;  // next node created at the same event (lookup chain)
+  uint32_t meta;       // [7:0] stage key, bit8 live, [31:16] live predecessor count
+};
+
+// ---- predecessor pointer (TimedKeyValue.Pointer): (version, key|null)
+struct Pred {
+  uint32_t prev;   // node index of the key, CEP_NONE = null key
+  uint32_t next;   // next Pred of the node, CEP_NONE = end
+  uint32_t removed;
+  uint32_t pad;
+  Dewey ver;
+};
+
+// ---- per-key state kept between kernel phases
+struct KeyState {
+  uint32_t n_matches;
+  uint32_t n_pairs;
+  uint32_t out_first;  // first output chunk (CEP_NONE: no output)
+  int32_t err;
+  uint32_t err_seq;
+  uint32_t pad[3];
+};
+
+constexpr uint32_t kOutChunkWords = 256;  // output stream chunk (last word links the next)
+
+// ---- interpreter bytecode (u32 words): op in [7:0], argument in [31:16]
+enum Bc : uint8_t {
+  BC_END = 0,
+  BC_PUSH32,   // + 1 word (sign-extended)
+  BC_PUSH64,   // + 2 words (lo, hi)
+  BC_FIELD,    // arg field
+  BC_TS,
+  BC_SGET,     // arg state, nullable
+  BC_SGETOR,   // arg state, pops the default
+  BC_CURR,     // nullable
+  BC_UNBOX,    // NPE if top is null
+  BC_ARITH,    // arg = op(0 add,1 sub,2 mul,3 div,4 rem) | type << 4
+  BC_NEG,      // arg type
+  BC_CAST,     // arg = from | to << 4
+  BC_CMP,      // arg = op(0 lt,1 le,2 gt,3 ge,4 eq,5 ne) | type << 4
+  BC_NOT,
+  BC_JF,       // arg = target word: top false -> jump keeping it, else pop
+  BC_JT,       // arg = target word: top true -> jump keeping it, else pop
+};
+
+}  // namespace cep

@@ -1,0 +1,682 @@
+// nfa.hip — the general NFA matching kernel (CEP_KIND_NFA) and its output compaction.
+//
+// One lane = one key = one reference NFA (nfa/NFA.java).  A 64-lane wavefront advances 64
+// keys in lockstep over their CSR event columns; each lane runs the reference's per-event
+// algorithm exactly (queue order, edge order, Dewey versions, buffer refcounts and
+// predecessor removal, fold timing), which is what makes the emitted match sets bit-exact.
+//
+//   per event j of key k                                   reference
+//   ------------------------------------------------------ -----------------------------------
+//   pop the |Q| runs present at event start, step each     NFA.matchPattern          :94-109
+//   step = evaluate(level 0) + begin re-add                NFA.matchPattern(ctx)    :139-160
+//   evaluate: edges, PROCEED chain (iterative), branch,    NFA.evaluate             :162-250
+//             folds on unwind
+//   dead run -> walk_remove (GC only)                      NFA.removePattern        :117-123
+//   finals -> walk_remove emitting the Sequence            NFA.matchConstruction    :111-115
+//   put / put(begin) / branch / peek(remove)               KVSharedVersionedBuffer :80-171
+//
+// State lives in HBM: the run FIFO is a per-key ring of Rec, buffer nodes and predecessor
+// pointers come from global pools (chunked per lane), matches stream into per-key chained
+// output chunks that the compaction kernels turn into flat, key-ordered arrays.
+#include <hip/hip_runtime.h>
+
+#include "cep_layout.h"
+#include "nfa_device.h"
+
+namespace cep {
+
+constexpr uint32_t kNoSk = 0xFF;
+
+template <int F>
+struct Lane {
+  const NfaArgs& A;
+  const DevQuery& q;
+  const uint32_t* code;
+  // key
+  uint32_t key;
+  uint64_t base;
+  uint32_t j;  // current event (sequence number within key)
+  Rec<F>* ring;
+  uint32_t head = 0, count = 0;
+  // pools
+  uint32_t ncur = 0, nend = 0, pcur = 0, pend = 0;
+  uint32_t ochunk = CEP_NONE, opos = 0;
+  uint32_t cur_first = CEP_NONE;  // node chain of event j
+  int err = KE_OK;
+  uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
+
+  __device__ Lane(const NfaArgs& a, const DevQuery& qq, const uint32_t* c) : A(a), q(qq), code(c) {}
+
+  __device__ __forceinline__ Rec<F>& R(uint32_t i) { return ring[i % A.rcap]; }
+
+  // ---------------------------------------------------------------- buffer nodes
+  __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
+    for (uint32_t i = first; i != CEP_NONE;) {
+      const Node& n = A.nodes[i];
+      if ((n.meta & 0xFF) == sk) return (n.meta & 0x100) ? i : CEP_NONE;
+      i = n.same_next;
+    }
+    return CEP_NONE;
+  }
+
+  __device__ uint32_t new_node(uint32_t sk) {
+    const uint32_t i = pool_take(A.node_pool, ncur, nend);
+    if (i == CEP_NONE) { err = KE_CAPACITY; return CEP_NONE; }
+    Node& n = A.nodes[i];
+    n.event = j;
+    n.refs = 1;
+    n.head = n.tail = CEP_NONE;
+    n.same_next = cur_first;
+    n.meta = sk | 0x100;
+    cur_first = i;
+    return i;
+  }
+
+  __device__ void append_pred(uint32_t node, uint32_t prev, const Dewey& v) {
+    const uint32_t p = pool_take(A.pred_pool, pcur, pend);
+    if (p == CEP_NONE) { err = KE_CAPACITY; return; }
+    Pred& e = A.preds[p];
+    e.prev = prev;
+    e.next = CEP_NONE;
+    e.removed = 0;
+    e.ver = v;
+    Node& n = A.nodes[node];
+    if (n.head == CEP_NONE) n.head = p;
+    else A.preds[n.tail].next = p;
+    n.tail = p;
+    n.meta += 1u << 16;
+  }
+
+  // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
+  __device__ void put_begin(uint32_t sk, const Dewey& v) {
+    uint32_t c = lookup(sk, cur_first);
+    if (c == CEP_NONE) {
+      c = new_node(sk);
+      if (err) return;
+    } else {
+      Node& n = A.nodes[c];
+      n.refs = 1;
+      n.head = n.tail = CEP_NONE;
+      n.meta = sk | 0x100;
+    }
+    append_pred(c, CEP_NONE, v);
+  }
+
+  // put(curr, currEvent, prev, prevEvent, version)  :80-97
+  __device__ void put_link(uint32_t sk, uint32_t prev_sk, uint32_t prev_ev, uint32_t prev_first,
+                           const Dewey& v) {
+    if (prev_sk == kNoSk) { put_begin(sk, v); return; }
+    if (prev_ev == CEP_NONE) { err = KE_NPE; return; }
+    const uint32_t p = lookup(prev_sk, prev_first);
+    if (p == CEP_NONE) { err = KE_ILLEGAL_STATE; return; }
+    uint32_t c = lookup(sk, cur_first);
+    if (c == CEP_NONE) {
+      c = new_node(sk);
+      if (err) return;
+    }
+    append_pred(c, p, v);
+  }
+
+  // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92
+  __device__ __forceinline__ uint32_t first_compat(uint32_t node, const Dewey& walker) {
+    for (uint32_t p = A.nodes[node].head; p != CEP_NONE; p = A.preds[p].next) {
+      const Pred& e = A.preds[p];
+      if (e.removed) continue;
+      if (dw_compatible(walker, e.ver)) return p;
+    }
+    return CEP_NONE;
+  }
+
+  // branch  :99-110
+  __device__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v) {
+    if (ev == CEP_NONE) { err = KE_NPE; return; }
+    uint32_t s = lookup(sk, first);
+    Dewey w = v;
+    for (;;) {
+      if (s == CEP_NONE || !(A.nodes[s].meta & 0x100)) { err = KE_NPE; return; }
+      A.nodes[s].refs += 1;
+      const uint32_t p = first_compat(s, w);
+      if (p == CEP_NONE) return;
+      const uint32_t nx = A.preds[p].prev;
+      if (nx == CEP_NONE) return;
+      w = A.preds[p].ver;
+      s = nx;
+    }
+  }
+
+  // ---------------------------------------------------------------- output stream
+  __device__ __forceinline__ uint32_t out_slot() {  // global word index of the next word
+    if (ochunk == CEP_NONE || opos == kOutChunkWords - 1) {
+      const uint32_t c = atomicAdd(A.out_pool.top, 1u);
+      if (c >= A.out_pool.cap) { err = KE_CAPACITY; return CEP_NONE; }
+      if (ochunk == CEP_NONE) out_first = c;
+      else A.out[(uint64_t)ochunk * kOutChunkWords + kOutChunkWords - 1] = c;
+      ochunk = c;
+      opos = 0;
+    }
+    return (uint32_t)0;  // unused
+  }
+  __device__ __forceinline__ uint64_t out_put(uint32_t w) {
+    out_slot();
+    if (err) return 0;
+    const uint64_t a = (uint64_t)ochunk * kOutChunkWords + opos++;
+    A.out[a] = w;
+    return a;
+  }
+
+  // peek(stage, event, version, remove=true)  :143-171; emit = match construction
+  __device__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit) {
+    if (ev == CEP_NONE) { err = KE_NPE; return; }
+    uint32_t s = lookup(sk, first);
+    Dewey w = v;
+    uint64_t npair_addr = 0;
+    uint32_t np = 0;
+    if (emit) {
+      out_put(j);
+      npair_addr = out_put(0);
+      if (err) return;
+    }
+    for (;;) {
+      if (s == CEP_NONE) { err = KE_NPE; return; }
+      Node& n = A.nodes[s];
+      const uint32_t meta = n.meta;
+      if (!(meta & 0x100)) { err = KE_NPE; return; }
+      const int32_t left = n.refs == 0 ? 0 : n.refs - 1;
+      n.refs = left;
+      uint32_t live_preds = meta >> 16;
+      if (left == 0 && live_preds <= 1) n.meta = meta & ~0x100u;  // store.delete
+      if (emit) {
+        out_put(n.event);
+        out_put(q.sk_name[meta & 0xFF]);
+        np++;
+        if (err) return;
+      }
+      const uint32_t p = first_compat(s, w);
+      if (p == CEP_NONE) break;
+      if (left == 0) {  // removePredecessor(pointer)
+        A.preds[p].removed = 1;
+        n.meta -= 1u << 16;
+      }
+      const uint32_t nx = A.preds[p].prev;
+      if (nx == CEP_NONE) break;
+      w = A.preds[p].ver;
+      s = nx;
+    }
+    if (emit) {
+      A.out[npair_addr] = np;
+      n_matches++;
+      n_pairs += np;
+    }
+  }
+
+  // ---------------------------------------------------------------- records
+  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {
+    return (sw & kRecEps) ? ((sw >> 8) & 0xFF) : q.st[sw & 0xFF].sk;
+  }
+  __device__ __forceinline__ bool rec_is_final(uint32_t sw) const {
+    return (sw & kRecEps) && q.st[sw & 0xFF].type == ST_FINAL;
+  }
+
+  __device__ Rec<F>* push_rec() {
+    if (count >= A.rcap) { err = KE_CAPACITY; return nullptr; }
+    Rec<F>* r = &R(head + count);
+    count++;
+    return r;
+  }
+
+  // ---------------------------------------------------------------- one run step
+  // Returns the number of records produced; -1 on error.  `c` was popped from the ring.
+  __device__ int step(const Rec<F>& c) {
+    int64_t W[F];
+#pragma unroll
+    for (int s = 0; s < F; s++) W[s] = c.fold[s];
+    uint32_t wnull = c.nullmask;
+    const uint32_t top = c.stage;
+    const bool top_eps = top & kRecEps;
+    const uint32_t top_sk = stage_sk(top);
+    int produced = 0;
+    Rec<F>* same_seq = nullptr;  // the (single) output record that keeps this run's sequence id
+
+    // level stack: cur stage, prev stage key, zeros appended, flags
+    uint8_t lv_cur[kMaxStages + 1];
+    uint8_t lv_prev[kMaxStages + 1];
+    uint8_t lv_zeros[kMaxStages + 1];
+    uint8_t lv_flags[kMaxStages + 1];  // 1 branching ctx, 2 br, 4 consumed, 8 ignored
+    int L = 0;
+    lv_cur[0] = (uint8_t)(top & 0xFF);
+    lv_prev[0] = kNoSk;
+    lv_zeros[0] = 0;
+    lv_flags[0] = (top & kRecBranch) ? 1 : 0;
+
+    EvalIn in;
+    in.cols = &A.cols;
+    in.ftype = q.field_type;
+    in.ts = A.ts;
+    in.pos = base + j;
+    in.W = W;
+    in.wnull = wnull;
+    in.curr = 0;
+    in.curr_null = true;
+
+    for (;;) {
+      const bool eps = (L == 0) && top_eps;
+      const uint32_t cur = lv_cur[L];
+      const uint32_t cur_sk = eps ? top_sk : q.st[cur].sk;
+      Dewey ver = c.ver;
+      for (int z = 0; z < lv_zeros[L]; z++)
+        if (!dw_add_stage(ver)) { err = KE_CAPACITY; return -1; }
+      uint32_t proceed_target = CEP_NONE;
+      if (eps) {
+        proceed_target = cur;  // epsilon: single PROCEED(true) -> target (Stage.java:42-46)
+      } else {
+        const DevStage& S = q.st[cur];
+        uint32_t matched = 0;
+        for (int e = 0; e < S.n_edges; e++) {  // matchEdgesAndGet :267-273 (all edges first)
+          bool hit = true;
+          if (S.e[e].prog != kProgTrue) {
+            bool rn;
+            int ee = 0;
+            const int64_t r = interp(code, S.e[e].prog, in, &rn, &ee);
+            if (ee) { err = ee; return -1; }
+            hit = r != 0;
+          }
+          if (hit) matched |= 1u << e;
+        }
+        uint32_t ops = 0;
+        for (int e = 0; e < S.n_edges; e++)
+          if (matched & (1u << e)) ops |= 1u << S.e[e].op;
+        const bool hasP = ops & (1u << OP_PROCEED), hasT = ops & (1u << OP_TAKE);
+        const bool hasI = ops & (1u << OP_IGNORE), hasB = ops & (1u << OP_BEGIN);
+        const bool br = (hasP && hasT) || (hasI && hasT) || (hasI && hasB) || (hasI && hasP);  // :280-289
+        if (br) lv_flags[L] |= 2;
+        for (int e = 0; e < S.n_edges; e++) {
+          if (!(matched & (1u << e))) continue;
+          const DevEdge E = S.e[e];
+          if (E.op == OP_PROCEED) {
+            proceed_target = E.target;
+          } else if (E.op == OP_TAKE) {
+            if (!br) {
+              Rec<F>* r = push_rec();
+              if (!r) return -1;
+              r->stage = kRecEps | (cur_sk << 8) | cur;  // newEpsilonState(current, current)
+              r->event = j;
+              r->ev_first = CEP_NONE;
+              r->ver = ver;
+              same_seq = r;
+              produced++;
+              put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
+            } else {
+              Dewey v2 = ver;
+              if (!dw_add_run(v2)) { err = KE_CAPACITY; return -1; }
+              put_link(cur_sk, lv_prev[L], c.event, c.ev_first, v2);
+            }
+            if (err) return -1;
+            lv_flags[L] |= 4;
+          } else if (E.op == OP_BEGIN) {
+            put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
+            if (err) return -1;
+            Rec<F>* r = push_rec();
+            if (!r) return -1;
+            uint32_t sw = kRecEps | (cur_sk << 8) | E.target;
+            if (q.st[E.target].type == ST_FINAL) sw |= kRecFinal;
+            r->stage = sw;
+            r->event = j;
+            r->ev_first = CEP_NONE;
+            r->ver = ver;
+            same_seq = r;
+            produced++;
+            lv_flags[L] |= 4;
+          } else {  // IGNORE
+            if (!br) {  // re-add the context record (top stage/event, this level's version)
+              Rec<F>* r = push_rec();
+              if (!r) return -1;
+              r->stage = (top & ~(kRecBranch | kRecFinal)) | ((lv_flags[L] & 1) ? kRecBranch : 0);
+              r->event = c.event;
+              r->ev_first = c.ev_first;
+              r->ver = ver;
+              same_seq = r;
+              produced++;
+            }
+            lv_flags[L] |= 8;
+          }
+        }
+      }
+      if (proceed_target == CEP_NONE) break;
+      // PROCEED: addStage unless the target is the same stage key or the run is branching
+      const uint32_t tsk = q.st[proceed_target].sk;
+      const bool branching = lv_flags[L] & 1;
+      const bool add = (tsk != cur_sk) && !branching;
+      if (L + 1 > kMaxStages) { err = KE_CAPACITY; return -1; }
+      lv_cur[L + 1] = (uint8_t)proceed_target;
+      lv_prev[L + 1] = (uint8_t)cur_sk;
+      lv_zeros[L + 1] = lv_zeros[L] + (add ? 1 : 0);
+      lv_flags[L + 1] = (add ? 0 : (branching ? 1 : 0));
+      L++;
+    }
+
+    // unwind: branch records and folds, deepest level first (recursion return order)
+    for (int l = L; l >= 0; l--) {
+      const uint8_t fl = lv_flags[l];
+      if (!(fl & 6)) continue;
+      const uint32_t cur = lv_cur[l];  // a real stage: epsilons never branch or consume
+      const DevStage& S = q.st[cur];
+      Dewey ver = c.ver;
+      for (int z = 0; z < lv_zeros[l]; z++) dw_add_stage(ver);
+      if (fl & 2) {  // isBranching :231-246
+        if (lv_prev[l] == kNoSk) { err = KE_NPE; return -1; }  // newEpsilonState(null, ...)
+        Rec<F>* r = push_rec();
+        if (!r) return -1;
+        r->stage = kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur;
+        if (fl & 8) {
+          r->event = c.event;
+          r->ev_first = c.ev_first;
+        } else {
+          r->event = j;
+          r->ev_first = CEP_NONE;
+        }
+        Dewey v2 = ver;
+        if (!dw_add_run(v2)) { err = KE_CAPACITY; return -1; }
+        r->ver = v2;
+        uint32_t nm = (1u << F) - 1;  // fresh sequence: only this stage's aggregates are copied
+        for (int a = 0; a < S.n_aggs; a++) {
+          const uint32_t s = S.agg_state[a];
+          if (!((wnull >> s) & 1u)) {
+            r->fold[s] = W[s];
+            nm &= ~(1u << s);
+          }
+        }
+        r->nullmask = nm;
+        produced++;
+        walk_branch(lv_prev[l], c.event, c.ev_first, ver);
+        if (err) return -1;
+      }
+      if (fl & 4) {  // evaluateAggregates :259-265, declaration order
+        for (int a = 0; a < S.n_aggs; a++) {
+          const uint32_t s = S.agg_state[a];
+          in.curr = W[s];
+          in.curr_null = (wnull >> s) & 1u;
+          bool rn;
+          int ee = 0;
+          const int64_t v = interp(code, S.agg_prog[a], in, &rn, &ee);
+          if (ee) { err = ee; return -1; }
+          W[s] = v;
+          wnull = rn ? (wnull | (1u << s)) : (wnull & ~(1u << s));
+        }
+      }
+    }
+    if (same_seq) {
+      for (int s = 0; s < F; s++) same_seq->fold[s] = W[s];
+      same_seq->nullmask = wnull;
+    }
+    // begin state re-added with a new run (:148-157)
+    if (!top_eps && q.st[top & 0xFF].type == ST_BEGIN) {
+      Rec<F>* r = push_rec();
+      if (!r) return -1;
+      r->stage = top & 0xFF;
+      r->event = CEP_NONE;
+      r->ev_first = CEP_NONE;
+      r->ver = c.ver;
+      if (produced > 0 && !dw_add_run(r->ver)) { err = KE_CAPACITY; return -1; }
+      r->nullmask = (1u << F) - 1;
+      produced++;
+    }
+    return produced;
+  }
+
+  // ---------------------------------------------------------------- one event
+  __device__ void event() {
+    cur_first = CEP_NONE;
+    const uint32_t n = count;
+    for (uint32_t i = 0; i < n; i++) {
+      const Rec<F> c = R(head);
+      head++;
+      count--;
+      const int produced = step(c);
+      if (err) return;
+      if (produced == 0) {  // removePattern
+        walk_remove(stage_sk(c.stage), c.event, c.ev_first, c.ver, false);
+        if (err) return;
+      }
+    }
+    // records created at this event learn the node chain of the event
+    for (uint32_t i = 0; i < count; i++) {
+      Rec<F>& r = R(head + i);
+      if (r.event == j) r.ev_first = cur_first;
+    }
+    // matchConstruction: finals in order, then drop them from the queue
+    bool any_final = false;
+    for (uint32_t i = 0; i < count; i++)
+      if (R(head + i).stage & kRecFinal) any_final = true;
+    if (!any_final) return;
+    const uint32_t m0 = n_matches, p0 = n_pairs;
+    uint32_t w = 0;
+    for (uint32_t i = 0; i < count; i++) {
+      const Rec<F> r = R(head + i);
+      if (r.stage & kRecFinal) {
+        walk_remove(stage_sk(r.stage), r.event, r.ev_first, r.ver, true);
+        if (err) { n_matches = m0; n_pairs = p0; return; }  // nothing of this event is forwarded
+      } else {
+        if (w != i) R(head + w) = r;
+        w++;
+      }
+    }
+    count = w;
+  }
+};
+
+template <int F>
+__global__ void __launch_bounds__(256) nfa_kernel(NfaArgs A) {
+  extern __shared__ uint32_t smem[];
+  DevQuery* qs = reinterpret_cast<DevQuery*>(smem);
+  uint32_t* code_s = smem + (sizeof(DevQuery) + 3) / 4;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(A.q);
+    for (uint32_t i = threadIdx.x; i < sizeof(DevQuery) / 4; i += blockDim.x) smem[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t code_len = qs->code_len;
+  for (uint32_t i = threadIdx.x; i < code_len; i += blockDim.x) code_s[i] = A.code[i];
+  __syncthreads();
+
+  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nslots = A.key_list ? A.n_list : A.n_keys;
+  if (slot >= nslots) return;
+  const uint32_t key = A.key_list ? A.key_list[slot] : (uint32_t)slot;
+
+  Lane<F> L(A, *qs, code_s);
+  L.key = key;
+  L.base = A.key_off[key];
+  const uint32_t n = (uint32_t)(A.key_off[key + 1] - L.base);
+  L.ring = reinterpret_cast<Rec<F>*>(A.rings) + slot * A.rcap;
+  // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
+  {
+    Rec<F>& r = L.ring[0];
+    r.stage = qs->begin_stage;
+    r.event = CEP_NONE;
+    r.ev_first = CEP_NONE;
+    r.nullmask = (1u << F) - 1;
+    dw_init(r.ver, 1);
+    L.head = 0;
+    L.count = 1;
+  }
+  uint32_t err_seq = 0;
+  for (uint32_t j = 0; j < n; j++) {
+    L.j = j;
+    L.event();
+    if (L.err) {
+      err_seq = j;
+      break;
+    }
+  }
+  KeyState& ks = A.ks[key];
+  ks.n_matches = L.n_matches;
+  ks.n_pairs = L.n_pairs;
+  ks.out_first = L.out_first;
+  ks.err = L.err;
+  ks.err_seq = err_seq;
+  if (L.err == KE_CAPACITY) atomicAdd(A.n_capacity_err, 1u);
+}
+
+// ---------------------------------------------------------------- compaction
+// exclusive scans of per-key match / pair counts (two-level: block sums, then offsets)
+__global__ void __launch_bounds__(256) count_blocks(const KeyState* ks, uint64_t n, uint64_t* bsum_m,
+                                                    uint64_t* bsum_p) {
+  __shared__ uint64_t sm[256], sp[256];
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  sm[threadIdx.x] = i < n ? ks[i].n_matches : 0;
+  sp[threadIdx.x] = i < n ? ks[i].n_pairs : 0;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sm[threadIdx.x] += sm[threadIdx.x + s];
+      sp[threadIdx.x] += sp[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bsum_m[blockIdx.x] = sm[0];
+    bsum_p[blockIdx.x] = sp[0];
+  }
+}
+
+// single block: in-place exclusive scan of nb block sums (sequential chunks per thread)
+__global__ void __launch_bounds__(1024) scan_blocks(uint64_t* bm, uint64_t* bp, uint64_t nb, uint64_t* totals) {
+  __shared__ uint64_t tm[1024], tp[1024];
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t a = threadIdx.x * per, b = (a + per < nb) ? a + per : nb;
+  uint64_t sm = 0, sp = 0;
+  for (uint64_t i = a; i < b; i++) { sm += bm[i]; sp += bp[i]; }
+  tm[threadIdx.x] = sm;
+  tp[threadIdx.x] = sp;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t am = 0, ap = 0;
+    for (int t = 0; t < 1024; t++) {
+      uint64_t xm = tm[t], xp = tp[t];
+      tm[t] = am;
+      tp[t] = ap;
+      am += xm;
+      ap += xp;
+    }
+    totals[0] = am;
+    totals[1] = ap;
+  }
+  __syncthreads();
+  uint64_t om = tm[threadIdx.x], op = tp[threadIdx.x];
+  for (uint64_t i = a; i < b; i++) {
+    uint64_t xm = bm[i], xp = bp[i];
+    bm[i] = om;
+    bp[i] = op;
+    om += xm;
+    op += xp;
+  }
+}
+
+// per key: walk the output chain and write flat arrays; digest = Σ hash(match)
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint64_t n, const uint64_t* bsum_m,
+                                                       const uint64_t* bsum_p, const uint32_t* out,
+                                                       uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
+                                                       uint32_t* p_seq, uint16_t* p_stage,
+                                                       const uint64_t* totals, unsigned long long* digest) {
+  __shared__ uint64_t sm[256], sp[256];
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nm = k < n ? ks[k].n_matches : 0, npairs = k < n ? ks[k].n_pairs : 0;
+  sm[threadIdx.x] = nm;
+  sp[threadIdx.x] = npairs;
+  __syncthreads();
+  // block-local exclusive scan (Hillis-Steele over 256)
+  for (int s = 1; s < 256; s <<= 1) {
+    uint64_t xm = threadIdx.x >= (unsigned)s ? sm[threadIdx.x - s] : 0;
+    uint64_t xp = threadIdx.x >= (unsigned)s ? sp[threadIdx.x - s] : 0;
+    __syncthreads();
+    sm[threadIdx.x] += xm;
+    sp[threadIdx.x] += xp;
+    __syncthreads();
+  }
+  uint64_t mo = bsum_m[blockIdx.x] + sm[threadIdx.x] - nm;
+  uint64_t po = bsum_p[blockIdx.x] + sp[threadIdx.x] - npairs;
+  if (k == 0) m_off[totals[0]] = totals[1];
+  if (nm == 0) return;
+  uint32_t chunk = ks[k].out_first, pos = 0;
+  uint64_t dsum = 0;
+  auto next = [&]() -> uint32_t {
+    if (pos == kOutChunkWords - 1) {
+      chunk = out[(uint64_t)chunk * kOutChunkWords + kOutChunkWords - 1];
+      pos = 0;
+    }
+    return out[(uint64_t)chunk * kOutChunkWords + pos++];
+  };
+  for (uint32_t m = 0; m < nm; m++) {
+    const uint32_t emit = next();
+    const uint32_t np = next();
+    m_key[mo] = (uint32_t)k;
+    m_emit[mo] = emit;
+    m_off[mo] = po;
+    uint64_t h = mix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)k << 32) ^ emit);
+    for (uint32_t i = 0; i < np; i++) {
+      const uint32_t s = next();
+      const uint32_t st = next();
+      p_seq[po] = s;
+      p_stage[po] = (uint16_t)st;
+      h = mix64(h ^ (((uint64_t)st << 32) | s));
+      po++;
+    }
+    dsum += h;
+    mo++;
+  }
+  atomicAdd(digest, (unsigned long long)dsum);
+}
+
+// ---------------------------------------------------------------- host launchers
+template <int F>
+static hipError_t launch_nfa_t(const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)((nslots + 255) / 256);
+  const size_t shm = ((sizeof(DevQuery) + 3) / 4 + code_len) * 4;
+  hipLaunchKernelGGL(nfa_kernel<F>, dim3(blocks), dim3(256), shm, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st) {
+  if (nslots == 0) return hipSuccess;
+  switch (F) {
+    case 0: case 1: case 2: return launch_nfa_t<2>(a, nslots, code_len, st);
+    case 3: case 4: return launch_nfa_t<4>(a, nslots, code_len, st);
+    default: return launch_nfa_t<8>(a, nslots, code_len, st);
+  }
+}
+
+size_t rec_size(int F) {
+  switch (F) {
+    case 0: case 1: case 2: return sizeof(Rec<2>);
+    case 3: case 4: return sizeof(Rec<4>);
+    default: return sizeof(Rec<8>);
+  }
+}
+
+hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
+                          uint64_t* totals, hipStream_t st) {
+  const uint64_t nb = (n_keys + 255) / 256;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(count_blocks, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p);
+  hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, st, bsum_m, bsum_p, nb, totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
+                          const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
+                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals,
+                          unsigned long long* digest, hipStream_t st) {
+  const uint64_t nb = (n_keys + 255) / 256;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_matches, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p, out,
+                     m_key, m_emit, m_off, p_seq, p_stage, totals, digest);
+  return hipGetLastError();
+}
+
+}  // namespace cep

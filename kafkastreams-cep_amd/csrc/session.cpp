@@ -1,0 +1,657 @@
+// session.cpp — the C ABI (include/cep.h): query compile, sessions on one GPU, batch
+// matching, result retrieval.  Host code; kernels live in nfa.hip / stencil.hip / synth.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cep_internal.h"
+#include "kernel_args.h"
+
+using namespace cep;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHECK(x)                                                                          \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess)                                                                    \
+      throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));                        \
+  } while (0)
+
+// A grow-only device buffer.
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t n) {
+    if (n <= bytes) return;
+    if (p) HIPCHECK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    n = std::max<size_t>(n, 256);
+    if (hipMalloc(&p, n) != hipSuccess) {
+      p = nullptr;
+      throw std::bad_alloc();
+    }
+    bytes = n;
+  }
+  // grow keeping the first `keep` bytes
+  void grow_keep(size_t n, size_t keep, hipStream_t st) {
+    if (n <= bytes) return;
+    void* q = nullptr;
+    if (hipMalloc(&q, n) != hipSuccess) throw std::bad_alloc();
+    if (p && keep) HIPCHECK(hipMemcpyAsync(q, p, std::min(keep, bytes), hipMemcpyDeviceToDevice, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (p) HIPCHECK(hipFree(p));
+    p = q;
+    bytes = n;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+template <class T> struct HVec {  // host copy of a result array
+  std::vector<T> v;
+};
+
+struct QueryRt {
+  const cep_query* q;
+  int F = 2;
+  DBuf d_q, d_code;
+  // results of the last batch (device)
+  DBuf m_key, m_emit, m_off, p_seq, p_stage;
+  DBuf ks;
+  uint64_t n_matches = 0, n_pairs = 0;
+  unsigned long long digest = 0;
+  uint32_t arity = 0;
+  bool have = false;
+  // host copies
+  std::vector<uint32_t> h_key, h_emit, h_seq;
+  std::vector<uint64_t> h_off;
+  std::vector<uint16_t> h_stage;
+  bool host_valid = false;
+  float kernel_ms = 0;
+  uint32_t launches = 0;
+};
+
+}  // namespace
+
+struct cep_session {
+  int device = 0;
+  cep_opts opts{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<std::unique_ptr<QueryRt>> qs;
+  // batch (device copies when the batch is host-resident)
+  DBuf b_off, b_ts;
+  DBuf b_cols[kMaxFields];
+  uint64_t n_keys = 0, n_events = 0;
+  const uint64_t* key_off = nullptr;
+  const int64_t* ts = nullptr;
+  Cols cols{};
+  int64_t watermark = INT64_MIN;
+  // scratch
+  DBuf rings, nodes, preds, out, scratch, tile_key, status, keylist;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int d) {
+    (void)hipGetDevice(&prev);
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+struct Scratch {  // small counters, one allocation
+  uint32_t node_top, pred_top, out_top, n_cap_err;
+  uint32_t tile_counter, overflow, pad0, pad1;
+  uint64_t totals[2];
+  uint64_t total;
+  unsigned long long digest;
+  unsigned long long wmax;
+};
+
+void run_stencil(cep_session* s, QueryRt& r) {
+  const cep_query* q = r.q;
+  const uint32_t m = q->info.arity;
+  const uint64_t n_tiles = stencil_tiles(s->n_events);
+  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));
+  s->status.ensure(sizeof(unsigned long long) * (n_tiles + 1));
+  s->scratch.ensure(sizeof(Scratch));
+  // worst case one match per event
+  const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
+  r.m_key.ensure(sizeof(uint32_t) * cap);
+  r.p_seq.ensure(sizeof(uint32_t) * cap * m);
+  Scratch* sc = s->scratch.as<Scratch>();
+  HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
+  HIPCHECK(hipMemsetAsync(s->status.p, 0, sizeof(unsigned long long) * (n_tiles + 1), s->stream));
+  StencilArgs a{};
+  a.n_keys = s->n_keys;
+  a.n_events = s->n_events;
+  a.key_off = s->key_off;
+  a.tile_key = s->tile_key.as<uint32_t>();
+  a.q = r.d_q.as<DevQuery>();
+  a.code = r.d_code.as<uint32_t>();
+  a.cols = s->cols;
+  a.ts = s->ts;
+  const bool range = q->stencilRange;
+  for (int c = 0; c < 2; c++) a.col[c] = (const int32_t*)s->cols.p[q->rangeCols[c]];
+  for (uint32_t i = 0; i < m && i < 8; i++) {
+    a.prog[i] = q->stencilProg[i];
+    for (int c = 0; c < 2; c++) {
+      a.rs[i].lo[c] = q->rangeLo[i][c];
+      a.rs[i].hi[c] = q->rangeHi[i][c];
+    }
+  }
+  for (uint32_t x = 0; x < m && x < 8; x++) a.stage_name[x] = q->arityStage[x];
+  a.tile_counter = &sc->tile_counter;
+  a.status = s->status.as<unsigned long long>();
+  a.m_key = r.m_key.as<uint32_t>();
+  a.p_seq = r.p_seq.as<uint32_t>();
+  a.total = &sc->total;
+  a.digest = &sc->digest;
+  a.out_cap = cap;
+  a.overflow = &sc->overflow;
+  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  HIPCHECK(launch_tile_first_key(s->key_off, s->n_keys, s->tile_key.as<uint32_t>(), s->n_events, s->stream));
+  HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->stream));
+  HIPCHECK(hipEventRecord(s->ev1, s->stream));
+  Scratch h{};
+  HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  HIPCHECK(hipEventElapsedTime(&r.kernel_ms, s->ev0, s->ev1));
+  r.launches = 2;
+  if (h.overflow) throw std::runtime_error("stencil output overflow");
+  r.n_matches = h.total;
+  r.n_pairs = h.total * m;
+  r.digest = h.digest;
+  r.arity = m;
+  // no per-key errors on this path: the predicates are total
+  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(s->n_keys, 1));
+  HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * s->n_keys, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+}
+
+void run_nfa(cep_session* s, QueryRt& r) {
+  const cep_query* q = r.q;
+  const uint64_t nk = s->n_keys;
+  uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
+  const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.25;
+  const size_t recsz = rec_size(r.F);
+  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
+  s->scratch.ensure(sizeof(Scratch));
+  Scratch* sc = s->scratch.as<Scratch>();
+
+  // pools: nodes / preds ~ pool_factor per event (+ chunk slack per key); output chunks
+  const uint32_t nchunk = 16, pchunk = 16;
+  uint64_t node_cap = (uint64_t)(pf * (double)s->n_events) + nk * nchunk + 4096;
+  uint64_t pred_cap = (uint64_t)(pf * (double)s->n_events) + nk * pchunk + 4096;
+  uint64_t out_cap = (uint64_t)(pf * (double)s->n_events * 2 / kOutChunkWords) + nk / 4 + 1024;
+  node_cap = std::min<uint64_t>(node_cap, 0xFFFFFFF0ull);
+  pred_cap = std::min<uint64_t>(pred_cap, 0xFFFFFFF0ull);
+  out_cap = std::min<uint64_t>(out_cap, 0xFFFFFFF0ull / kOutChunkWords);
+  s->nodes.ensure(sizeof(Node) * node_cap);
+  s->preds.ensure(sizeof(Pred) * pred_cap);
+  s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
+  s->rings.ensure(recsz * rcap * std::max<uint64_t>(nk, 1));
+  HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
+
+  NfaArgs a{};
+  a.q = r.d_q.as<DevQuery>();
+  a.code = r.d_code.as<uint32_t>();
+  a.n_keys = nk;
+  a.key_off = s->key_off;
+  a.cols = s->cols;
+  a.ts = s->ts;
+  a.rings = s->rings.p;
+  a.rcap = rcap;
+  a.key_list = nullptr;
+  a.n_list = 0;
+  a.nodes = s->nodes.as<Node>();
+  a.preds = s->preds.as<Pred>();
+  a.out = s->out.as<uint32_t>();
+  a.node_pool = Pool{&sc->node_top, (uint32_t)node_cap, nchunk};
+  a.pred_pool = Pool{&sc->pred_top, (uint32_t)pred_cap, pchunk};
+  a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, 1};
+  a.ks = r.ks.as<KeyState>();
+  a.n_capacity_err = &sc->n_cap_err;
+
+  float total_ms = 0;
+  r.launches = 0;
+  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  HIPCHECK(launch_nfa(r.F, a, nk, q->dev.code_len, s->stream));
+  HIPCHECK(hipEventRecord(s->ev1, s->stream));
+  r.launches++;
+  Scratch h{};
+  HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  float ms = 0;
+  HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+  total_ms += ms;
+
+  // retry keys that hit a capacity limit with 8x the live-run ring and grown pools
+  for (int round = 0; h.n_cap_err > 0 && round < 3; round++) {
+    std::vector<KeyState> hks(nk);
+    HIPCHECK(hipMemcpyAsync(hks.data(), r.ks.p, sizeof(KeyState) * nk, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    std::vector<uint32_t> list;
+    for (uint64_t k = 0; k < nk; k++)
+      if (hks[k].err == KE_CAPACITY) list.push_back((uint32_t)k);
+    if (list.empty()) break;
+    rcap *= 8;
+    s->keylist.ensure(sizeof(uint32_t) * list.size());
+    HIPCHECK(hipMemcpyAsync(s->keylist.p, list.data(), sizeof(uint32_t) * list.size(), hipMemcpyHostToDevice,
+                            s->stream));
+    // grow pools (indices stay valid: copy the used prefix)
+    const uint64_t extra_events = 0;
+    (void)extra_events;
+    uint64_t nn = std::min<uint64_t>(node_cap * 2 + (uint64_t)list.size() * 4096, 0xFFFFFFF0ull);
+    uint64_t pn = std::min<uint64_t>(pred_cap * 2 + (uint64_t)list.size() * 4096, 0xFFFFFFF0ull);
+    uint64_t on = std::min<uint64_t>(out_cap * 2 + (uint64_t)list.size() * 64, 0xFFFFFFF0ull / kOutChunkWords);
+    s->nodes.grow_keep(sizeof(Node) * nn, sizeof(Node) * std::min<uint64_t>(h.node_top, node_cap), s->stream);
+    s->preds.grow_keep(sizeof(Pred) * pn, sizeof(Pred) * std::min<uint64_t>(h.pred_top, pred_cap), s->stream);
+    s->out.grow_keep(sizeof(uint32_t) * kOutChunkWords * on,
+                     sizeof(uint32_t) * kOutChunkWords * std::min<uint64_t>(h.out_top, out_cap), s->stream);
+    Scratch fix = h;  // pool tops may have run past the caps; restart them at the old caps
+    fix.node_top = (uint32_t)std::min<uint64_t>(h.node_top, node_cap);
+    fix.pred_top = (uint32_t)std::min<uint64_t>(h.pred_top, pred_cap);
+    fix.out_top = (uint32_t)std::min<uint64_t>(h.out_top, out_cap);
+    fix.n_cap_err = 0;
+    node_cap = nn;
+    pred_cap = pn;
+    out_cap = on;
+    DBuf retry_rings;
+    retry_rings.ensure(recsz * rcap * list.size());
+    HIPCHECK(hipMemcpyAsync(sc, &fix, sizeof fix, hipMemcpyHostToDevice, s->stream));
+    a.nodes = s->nodes.as<Node>();
+    a.preds = s->preds.as<Pred>();
+    a.out = s->out.as<uint32_t>();
+    a.node_pool.cap = (uint32_t)node_cap;
+    a.pred_pool.cap = (uint32_t)pred_cap;
+    a.out_pool.cap = (uint32_t)out_cap;
+    a.rings = retry_rings.p;
+    a.rcap = rcap;
+    a.key_list = s->keylist.as<uint32_t>();
+    a.n_list = (uint32_t)list.size();
+    HIPCHECK(hipEventRecord(s->ev0, s->stream));
+    HIPCHECK(launch_nfa(r.F, a, list.size(), q->dev.code_len, s->stream));
+    HIPCHECK(hipEventRecord(s->ev1, s->stream));
+    r.launches++;
+    HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    total_ms += ms;
+  }
+
+  // compaction: scans of per-key counts, then the scatter into flat arrays
+  const uint64_t nb = (nk + 255) / 256;
+  DBuf bsum;
+  bsum.ensure(sizeof(uint64_t) * 2 * (nb + 1));
+  uint64_t* bm = bsum.as<uint64_t>();
+  uint64_t* bp = bm + nb + 1;
+  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  HIPCHECK(launch_compact(r.ks.as<KeyState>(), nk, bm, bp, sc->totals, s->stream));
+  uint64_t tot[2] = {0, 0};
+  HIPCHECK(hipMemcpyAsync(tot, sc->totals, sizeof tot, hipMemcpyDeviceToHost, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  r.n_matches = tot[0];
+  r.n_pairs = tot[1];
+  r.m_key.ensure(sizeof(uint32_t) * (tot[0] + 1));
+  r.m_emit.ensure(sizeof(uint32_t) * (tot[0] + 1));
+  r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));
+  r.p_seq.ensure(sizeof(uint32_t) * (tot[1] + 1));
+  r.p_stage.ensure(sizeof(uint16_t) * (tot[1] + 1));
+  HIPCHECK(launch_scatter(r.ks.as<KeyState>(), nk, bm, bp, s->out.as<uint32_t>(), r.m_key.as<uint32_t>(),
+                          r.m_emit.as<uint32_t>(), r.m_off.as<uint64_t>(), r.p_seq.as<uint32_t>(),
+                          r.p_stage.as<uint16_t>(), sc->totals, &sc->digest, s->stream));
+  if (nk == 0) HIPCHECK(hipMemsetAsync(r.m_off.p, 0, sizeof(uint64_t), s->stream));
+  HIPCHECK(hipEventRecord(s->ev1, s->stream));
+  HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+  total_ms += ms;
+  r.launches += 3;
+  r.digest = h.digest;
+  r.arity = 0;
+  r.kernel_ms = total_ms;
+}
+
+int guarded(const std::function<void()>& f) {
+  try {
+    f();
+    return CEP_OK;
+  } catch (HipError& e) {
+    return fail(CEP_E_HIP, e.what());
+  } catch (std::bad_alloc&) {
+    return fail(CEP_E_NOMEM, "device allocation failed");
+  } catch (std::exception& e) {
+    return fail(CEP_E_INVALID, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cep_last_error(void) { return g_err.c_str(); }
+
+int cep_query_compile(const uint8_t* ir, size_t n, cep_query** out) {
+  if (!ir || !out) return fail(CEP_E_INVALID, "null argument");
+  auto q = std::make_unique<cep_query>();
+  try {
+    compile_query(ir, n, q.get());
+  } catch (std::exception& e) {
+    return fail(CEP_E_COMPILE, e.what());
+  }
+  *out = q.release();
+  return CEP_OK;
+}
+
+int cep_query_info_get(const cep_query* q, cep_query_info* info) {
+  if (!q || !info) return fail(CEP_E_INVALID, "null argument");
+  *info = q->info;
+  return CEP_OK;
+}
+
+const char* cep_query_stage_name(const cep_query* q, uint32_t id) {
+  if (!q || id >= q->names.size()) return nullptr;
+  return q->names[id].c_str();
+}
+
+void cep_query_destroy(cep_query* q) { delete q; }
+
+int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts, cep_session** out) {
+  if (!queries || n_queries <= 0 || !out) return fail(CEP_E_INVALID, "need at least one query");
+  for (int i = 0; i < n_queries; i++) {
+    if (!queries[i]) return fail(CEP_E_INVALID, "null query");
+    if (queries[i]->info.compile_error)
+      return fail(CEP_E_COMPILE, "query " + std::to_string(i) + " does not compile in the reference");
+    if (queries[i]->info.n_fields != queries[0]->info.n_fields)
+      return fail(CEP_E_INVALID, "queries of a session must share the event schema");
+  }
+  auto s = std::make_unique<cep_session>();
+  if (opts) s->opts = *opts;
+  s->device = s->opts.device;
+  int rc = guarded([&] {
+    DeviceGuard g(s->device);
+    HIPCHECK(hipSetDevice(s->device));
+    HIPCHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreate(&s->ev0));
+    HIPCHECK(hipEventCreate(&s->ev1));
+    for (int i = 0; i < n_queries; i++) {
+      auto r = std::make_unique<QueryRt>();
+      r->q = queries[i];
+      const uint32_t ns = queries[i]->info.n_states;
+      r->F = ns <= 2 ? 2 : ns <= 4 ? 4 : 8;
+      r->d_q.ensure(sizeof(DevQuery));
+      HIPCHECK(hipMemcpy(r->d_q.p, &queries[i]->dev, sizeof(DevQuery), hipMemcpyHostToDevice));
+      r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());
+      HIPCHECK(hipMemcpy(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
+                         hipMemcpyHostToDevice));
+      s->qs.push_back(std::move(r));
+    }
+  });
+  if (rc) return rc;
+  *out = s.release();
+  return CEP_OK;
+}
+
+void cep_session_destroy(cep_session* s) {
+  if (!s) return;
+  {
+    DeviceGuard g(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    s->qs.clear();
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+  }
+  delete s;
+}
+
+int cep_push_batch(cep_session* s, const cep_batch* b) {
+  if (!s || !b || !b->key_off || (!b->cols && b->n_events)) return fail(CEP_E_INVALID, "null argument");
+  if (b->n_keys >= 0xFFFFFFFFull || b->n_events >= 0xFFFFFFFFull)
+    return fail(CEP_E_INVALID, "a batch holds < 2^32 keys and events (sequence numbers are u32)");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    const cep_query* q0 = s->qs[0]->q;
+    const uint32_t nf = q0->info.n_fields;
+    s->n_keys = b->n_keys;
+    s->n_events = b->n_events;
+    for (auto& r : s->qs) {
+      r->have = false;
+      r->host_valid = false;
+    }
+    if (b->memory == CEP_MEM_DEVICE) {
+      s->key_off = b->key_off;
+      for (uint32_t f = 0; f < nf; f++) s->cols.p[f] = b->cols[f];
+      s->ts = b->ts;
+    } else {
+      s->b_off.ensure(sizeof(uint64_t) * (b->n_keys + 1));
+      HIPCHECK(hipMemcpyAsync(s->b_off.p, b->key_off, sizeof(uint64_t) * (b->n_keys + 1), hipMemcpyHostToDevice,
+                              s->stream));
+      s->key_off = s->b_off.as<uint64_t>();
+      for (uint32_t f = 0; f < nf; f++) {
+        const size_t esz = q0->dev.field_type[f] == 1 ? 4 : 8;
+        s->b_cols[f].ensure(esz * std::max<uint64_t>(b->n_events, 1));
+        if (b->n_events)
+          HIPCHECK(hipMemcpyAsync(s->b_cols[f].p, b->cols[f], esz * b->n_events, hipMemcpyHostToDevice, s->stream));
+        s->cols.p[f] = s->b_cols[f].p;
+      }
+      if (b->ts) {
+        s->b_ts.ensure(sizeof(int64_t) * std::max<uint64_t>(b->n_events, 1));
+        HIPCHECK(hipMemcpyAsync(s->b_ts.p, b->ts, sizeof(int64_t) * b->n_events, hipMemcpyHostToDevice, s->stream));
+        s->ts = s->b_ts.as<int64_t>();
+      } else {
+        s->ts = nullptr;
+      }
+    }
+    // watermark
+    s->watermark = INT64_MIN;
+    if (s->ts && s->n_events) {
+      s->scratch.ensure(sizeof(Scratch));
+      Scratch* sc = s->scratch.as<Scratch>();
+      HIPCHECK(hipMemsetAsync(&sc->wmax, 0, sizeof(unsigned long long), s->stream));
+      HIPCHECK(launch_max(s->ts, s->n_events, &sc->wmax, s->stream));
+      unsigned long long w = 0;
+      HIPCHECK(hipMemcpyAsync(&w, &sc->wmax, sizeof w, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipStreamSynchronize(s->stream));
+      s->watermark = (int64_t)(w ^ 0x8000000000000000ull);
+    }
+    for (auto& r : s->qs) {
+      if (r->q->info.kind == CEP_KIND_STENCIL && !s->opts.force_nfa) run_stencil(s, *r);
+      else run_nfa(s, *r);
+      r->have = true;
+    }
+  });
+}
+
+int cep_sync(cep_session* s) {
+  if (!s) return fail(CEP_E_INVALID, "null session");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    HIPCHECK(hipStreamSynchronize(s->stream));
+  });
+}
+
+int cep_poll_matches(cep_session* s, int query, int memory, cep_matches* out) {
+  if (!s || !out || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  QueryRt& r = *s->qs[query];
+  if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    std::memset(out, 0, sizeof *out);
+    out->n_matches = r.n_matches;
+    out->n_pairs = r.n_pairs;
+    out->arity = r.arity;
+    out->arity_stage = r.arity ? r.q->arityStage.data() : nullptr;
+    out->memory = memory;
+    if (memory == CEP_MEM_DEVICE) {
+      out->key = r.m_key.as<uint32_t>();
+      out->emit_seq = r.arity ? nullptr : r.m_emit.as<uint32_t>();
+      out->pair_off = r.arity ? nullptr : r.m_off.as<uint64_t>();
+      out->pair_seq = r.p_seq.as<uint32_t>();
+      out->pair_stage = r.arity ? nullptr : r.p_stage.as<uint16_t>();
+      return;
+    }
+    if (!r.host_valid) {
+      r.h_key.resize(r.n_matches);
+      r.h_seq.resize(r.n_pairs);
+      if (r.n_matches)
+        HIPCHECK(hipMemcpyAsync(r.h_key.data(), r.m_key.p, 4 * r.n_matches, hipMemcpyDeviceToHost, s->stream));
+      if (r.n_pairs)
+        HIPCHECK(hipMemcpyAsync(r.h_seq.data(), r.p_seq.p, 4 * r.n_pairs, hipMemcpyDeviceToHost, s->stream));
+      if (!r.arity) {
+        r.h_emit.resize(r.n_matches);
+        r.h_off.resize(r.n_matches + 1);
+        r.h_stage.resize(r.n_pairs);
+        if (r.n_matches)
+          HIPCHECK(hipMemcpyAsync(r.h_emit.data(), r.m_emit.p, 4 * r.n_matches, hipMemcpyDeviceToHost, s->stream));
+        HIPCHECK(hipMemcpyAsync(r.h_off.data(), r.m_off.p, 8 * (r.n_matches + 1), hipMemcpyDeviceToHost, s->stream));
+        if (r.n_pairs)
+          HIPCHECK(hipMemcpyAsync(r.h_stage.data(), r.p_stage.p, 2 * r.n_pairs, hipMemcpyDeviceToHost, s->stream));
+      }
+      HIPCHECK(hipStreamSynchronize(s->stream));
+      r.host_valid = true;
+    }
+    out->key = r.h_key.data();
+    out->pair_seq = r.h_seq.data();
+    if (!r.arity) {
+      out->emit_seq = r.h_emit.data();
+      out->pair_off = r.h_off.data();
+      out->pair_stage = r.h_stage.data();
+    }
+  });
+}
+
+int cep_key_errors(cep_session* s, int query, int32_t* code, uint32_t* seq, uint64_t n_keys) {
+  if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  QueryRt& r = *s->qs[query];
+  if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
+  if (n_keys > s->n_keys) return fail(CEP_E_INVALID, "n_keys larger than the batch");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    std::vector<KeyState> ks(n_keys);
+    if (n_keys)
+      HIPCHECK(hipMemcpyAsync(ks.data(), r.ks.p, sizeof(KeyState) * n_keys, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    for (uint64_t k = 0; k < n_keys; k++) {
+      if (code) code[k] = ks[k].err;
+      if (seq) seq[k] = ks[k].err_seq;
+    }
+  });
+}
+
+int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* checksum) {
+  if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  QueryRt& r = *s->qs[query];
+  if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
+  if (n_matches) *n_matches = r.n_matches;
+  if (checksum) *checksum = r.digest;
+  return CEP_OK;
+}
+
+int cep_watermark(cep_session* s, int64_t* out) {
+  if (!s || !out) return fail(CEP_E_INVALID, "null argument");
+  *out = s->watermark;
+  return CEP_OK;
+}
+
+int cep_last_timing(cep_session* s, int query, double* kernel_ms, uint32_t* launches) {
+  if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  if (kernel_ms) *kernel_ms = s->qs[query]->kernel_ms;
+  if (launches) *launches = s->qs[query]->launches;
+  return CEP_OK;
+}
+
+int cep_alloc_pinned(size_t bytes, void** out) {
+  if (!out) return fail(CEP_E_INVALID, "null argument");
+  return guarded([&] { HIPCHECK(hipHostMalloc(out, bytes, hipHostMallocDefault)); });
+}
+
+int cep_free_pinned(void* p) {
+  return guarded([&] { HIPCHECK(hipHostFree(p)); });
+}
+
+int cep_device_alloc(int device, size_t bytes, void** out) {
+  if (!out) return fail(CEP_E_INVALID, "null argument");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(hipMalloc(out, std::max<size_t>(bytes, 256)));
+  });
+}
+
+int cep_device_free(void* p) {
+  return guarded([&] { HIPCHECK(hipFree(p)); });
+}
+
+int cep_memcpy(void* dst, const void* src, size_t bytes, int dst_memory, int src_memory) {
+  hipMemcpyKind k = dst_memory == CEP_MEM_DEVICE ? (src_memory == CEP_MEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                                                  : hipMemcpyHostToDevice)
+                                                 : (src_memory == CEP_MEM_DEVICE ? hipMemcpyDeviceToHost
+                                                                                  : hipMemcpyHostToHost);
+  return guarded([&] { HIPCHECK(hipMemcpy(dst, src, bytes, k)); });
+}
+
+// ---- synthetic workloads ----
+static std::vector<uint64_t> synth_offsets(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
+                                           uint32_t mean) {
+  (void)kind;
+  std::vector<uint64_t> off(n_keys + 1, 0);
+  const uint64_t sp = (uint64_t)std::floor(std::sqrt((double)mean));
+  for (uint64_t k = 0; k < n_keys; k++) {
+    const uint64_t h = cep::synth_hash_host(seed, k + key_base, 0xFFFFFFFFull);
+    off[k + 1] = off[k] + (mean - sp + h % (2 * sp + 1));
+  }
+  return off;
+}
+
+int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, uint32_t mean_events,
+                    uint64_t* n_events) {
+  (void)device;
+  if (!n_events || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
+  *n_events = synth_offsets(kind, seed, n_keys, key_base, mean_events)[n_keys];
+  return CEP_OK;
+}
+
+int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, uint32_t mean_events,
+                       uint64_t* key_off_dev, int32_t* const* cols_dev) {
+  if (!key_off_dev || !cols_dev || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
+  if (kind != 0 && kind != 1) return fail(CEP_E_INVALID, "kind must be 0 (abc) or 1 (stock)");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    auto off = synth_offsets(kind, seed, n_keys, key_base, mean_events);
+    HIPCHECK(hipMemcpy(key_off_dev, off.data(), sizeof(uint64_t) * (n_keys + 1), hipMemcpyHostToDevice));
+    HIPCHECK(launch_synth(kind, seed, n_keys, key_base, key_off_dev, cols_dev[0], kind == 1 ? cols_dev[1] : nullptr,
+                          nullptr));
+    HIPCHECK(hipDeviceSynchronize());
+  });
+}
+
+}  // extern "C"

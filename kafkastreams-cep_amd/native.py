@@ -1,0 +1,282 @@
+"""ctypes binding of libcep.so (include/cep.h) — the product path.
+
+There is no fallback: if libcep.so is missing or no GPU is visible, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcep.so")
+
+CEP_MEM_HOST, CEP_MEM_DEVICE = 0, 1
+CEP_KIND_NFA, CEP_KIND_STENCIL = 0, 1
+KEY_ERRORS = {0: None, 1: "NullPointerException", 2: "IllegalStateException",
+              3: "ArithmeticException", 16: "capacity"}
+
+# every symbol include/cep.h declares (tests check the library exports them all)
+EXPORTS = [
+    "cep_query_compile", "cep_query_info_get", "cep_query_stage_name", "cep_query_destroy",
+    "cep_session_create", "cep_session_destroy", "cep_push_batch", "cep_sync", "cep_poll_matches",
+    "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
+    "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
+    "cep_synth_count", "cep_synth_generate",
+]
+
+
+class QueryInfo(C.Structure):
+    _fields_ = [("n_patterns", C.c_uint32), ("n_stages", C.c_uint32), ("n_names", C.c_uint32),
+                ("n_fields", C.c_uint32), ("n_states", C.c_uint32), ("kind", C.c_uint32),
+                ("arity", C.c_uint32), ("compile_error", C.c_int32)]
+
+
+class Opts(C.Structure):
+    _fields_ = [("device", C.c_int), ("force_nfa", C.c_int), ("max_runs", C.c_uint32),
+                ("pool_factor", C.c_double)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_keys", C.c_uint64), ("n_events", C.c_uint64), ("key_off", C.c_void_p),
+                ("cols", C.POINTER(C.c_void_p)), ("ts", C.c_void_p), ("memory", C.c_int)]
+
+
+class Matches(C.Structure):
+    _fields_ = [("n_matches", C.c_uint64), ("n_pairs", C.c_uint64), ("arity", C.c_uint32),
+                ("arity_stage", C.POINTER(C.c_uint16)), ("key", C.POINTER(C.c_uint32)),
+                ("emit_seq", C.POINTER(C.c_uint32)), ("pair_off", C.POINTER(C.c_uint64)),
+                ("pair_seq", C.POINTER(C.c_uint32)), ("pair_stage", C.POINTER(C.c_uint16)),
+                ("memory", C.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32
+        sig = {
+            "cep_query_compile": ([C.c_char_p, C.c_size_t, C.POINTER(vp)], C.c_int),
+            "cep_query_info_get": ([vp, C.POINTER(QueryInfo)], C.c_int),
+            "cep_query_stage_name": ([vp, u32], C.c_char_p),
+            "cep_query_destroy": ([vp], None),
+            "cep_session_create": ([C.POINTER(vp), C.c_int, C.POINTER(Opts), C.POINTER(vp)], C.c_int),
+            "cep_session_destroy": ([vp], None),
+            "cep_push_batch": ([vp, C.POINTER(Batch)], C.c_int),
+            "cep_sync": ([vp], C.c_int),
+            "cep_poll_matches": ([vp, C.c_int, C.c_int, C.POINTER(Matches)], C.c_int),
+            "cep_key_errors": ([vp, C.c_int, C.POINTER(i32), C.POINTER(u32), u64], C.c_int),
+            "cep_match_digest": ([vp, C.c_int, C.POINTER(u64), C.POINTER(u64)], C.c_int),
+            "cep_watermark": ([vp, C.POINTER(C.c_int64)], C.c_int),
+            "cep_last_timing": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(u32)], C.c_int),
+            "cep_last_error": ([], C.c_char_p),
+            "cep_device_alloc": ([C.c_int, C.c_size_t, C.POINTER(vp)], C.c_int),
+            "cep_device_free": ([vp], C.c_int),
+            "cep_memcpy": ([vp, vp, C.c_size_t, C.c_int, C.c_int], C.c_int),
+            "cep_synth_count": ([C.c_int, C.c_int, u64, u64, u64, u32, C.POINTER(u64)], C.c_int),
+            "cep_synth_generate": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes, f.restype = args, res
+        _lib = L
+    return _lib
+
+
+class CepError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise CepError(f"libcep error {rc}: {lib().cep_last_error().decode(errors='replace')}")
+
+
+class Query:
+    """A compiled query (cep_query_compile ~ StatesFactory.make)."""
+
+    def __init__(self, ir: bytes):
+        self.ir = ir
+        h = C.c_void_p()
+        _check(lib().cep_query_compile(ir, len(ir), C.byref(h)))
+        self.h = h
+        self.info = QueryInfo()
+        _check(lib().cep_query_info_get(self.h, C.byref(self.info)))
+        self.stage_names = [lib().cep_query_stage_name(self.h, i).decode() for i in range(self.info.n_names)]
+
+    @property
+    def kind(self):
+        return self.info.kind
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.cep_query_destroy(self.h)
+            self.h = None
+
+
+class DeviceBuffer:
+    def __init__(self, nbytes: int, device: int = 0):
+        self.nbytes, self.device = int(nbytes), device
+        p = C.c_void_p()
+        _check(lib().cep_device_alloc(device, max(1, self.nbytes), C.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(lib().cep_memcpy(self.ptr, arr.ctypes.data, arr.nbytes, CEP_MEM_DEVICE, CEP_MEM_HOST))
+
+    def download(self, dtype, count) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            _check(lib().cep_memcpy(out.ctypes.data, self.ptr, out.nbytes, CEP_MEM_HOST, CEP_MEM_DEVICE))
+        return out
+
+    def free(self):
+        if self.ptr and _lib is not None:
+            _lib.cep_device_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+class DeviceStream:
+    """A device-resident CSR batch (key_off u64 + int32 columns)."""
+
+    def __init__(self, n_keys, n_events, key_off: DeviceBuffer, cols: list, device=0, keep=None):
+        self.n_keys, self.n_events = int(n_keys), int(n_events)
+        self.key_off, self.cols, self.device = key_off, cols, device
+        self._keep = keep
+
+    @classmethod
+    def from_host(cls, key_off, cols, device=0):
+        key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+        kb = DeviceBuffer(key_off.nbytes, device)
+        kb.upload(key_off)
+        cbs = []
+        for c in cols:
+            c = np.ascontiguousarray(c)
+            b = DeviceBuffer(c.nbytes, device)
+            b.upload(c)
+            cbs.append(b)
+        return cls(len(key_off) - 1, int(key_off[-1]), kb, cbs, device)
+
+    def download(self):
+        off = self.key_off.download(np.uint64, self.n_keys + 1)
+        cols = [c.download(np.int32, self.n_events) for c in self.cols]
+        return off, cols
+
+
+def synth_stream(kind: str, seed: int, n_keys: int, mean_events: int, key_base: int = 0,
+                 device: int = 0) -> DeviceStream:
+    """Generate workloads.SynthConfig data directly in HBM (csrc/synth.hip)."""
+    k = {"abc": 0, "stock": 1}[kind]
+    n = C.c_uint64()
+    _check(lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
+    off = DeviceBuffer(8 * (n_keys + 1), device)
+    ncols = 1 if k == 0 else 2
+    cols = [DeviceBuffer(4 * max(1, n.value), device) for _ in range(ncols)]
+    ptrs = (C.c_void_p * ncols)(*[c.ptr for c in cols])
+    _check(lib().cep_synth_generate(device, k, seed, n_keys, key_base, mean_events, off.ptr, ptrs))
+    return DeviceStream(n_keys, n.value, off, cols, device)
+
+
+class Session:
+    """cep_session: per-key NFA state for one or more queries on one GPU."""
+
+    def __init__(self, queries, device: int = 0, force_nfa: bool = False, max_runs: int = 0,
+                 pool_factor: float = 0.0):
+        if isinstance(queries, Query):
+            queries = [queries]
+        self.queries = list(queries)
+        arr = (C.c_void_p * len(self.queries))(*[q.h.value for q in self.queries])
+        opts = Opts(device, 1 if force_nfa else 0, max_runs, pool_factor)
+        h = C.c_void_p()
+        _check(lib().cep_session_create(arr, len(self.queries), C.byref(opts), C.byref(h)))
+        self.h = h
+        self.device = device
+        self.n_keys = 0
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.cep_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # -- input --
+    def push(self, key_off, cols, ts=None):
+        """Host numpy CSR batch."""
+        key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        tsp = None
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, dtype=np.int64)
+            tsp = ts.ctypes.data
+        b = Batch(len(key_off) - 1, int(key_off[-1]) if len(key_off) else 0, key_off.ctypes.data,
+                  ptrs, tsp, CEP_MEM_HOST)
+        _check(lib().cep_push_batch(self.h, C.byref(b)))
+        self.n_keys = len(key_off) - 1
+
+    def push_device(self, stream: DeviceStream, ts_ptr=None):
+        ptrs = (C.c_void_p * len(stream.cols))(*[c.ptr for c in stream.cols])
+        b = Batch(stream.n_keys, stream.n_events, stream.key_off.ptr, ptrs, ts_ptr, CEP_MEM_DEVICE)
+        _check(lib().cep_push_batch(self.h, C.byref(b)))
+        self.n_keys = stream.n_keys
+
+    # -- output --
+    def matches(self, query: int = 0) -> dict:
+        """Host copy of the last batch's matches, always in variable-length form."""
+        m = Matches()
+        _check(lib().cep_poll_matches(self.h, query, CEP_MEM_HOST, C.byref(m)))
+        nm, npairs = m.n_matches, m.n_pairs
+
+        def arr(p, n, dt):
+            return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True) if n else np.zeros(0, dt)
+
+        key = arr(m.key, nm, np.uint32)
+        seq = arr(m.pair_seq, npairs, np.uint32)
+        if m.arity:
+            a = m.arity
+            stages = np.array([m.arity_stage[i] for i in range(a)], dtype=np.uint16)
+            emit = seq[0::a].copy() if nm else np.zeros(0, np.uint32)
+            off = (np.arange(nm + 1, dtype=np.uint64) * a)
+            stage = np.tile(stages, nm)
+        else:
+            emit = arr(m.emit_seq, nm, np.uint32)
+            off = arr(m.pair_off, nm + 1, np.uint64)
+            stage = arr(m.pair_stage, npairs, np.uint16)
+        return {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
+                "pair_seq": seq, "pair_stage": stage, "arity": m.arity}
+
+    def key_errors(self, query: int = 0, n_keys: int | None = None):
+        n = self.n_keys if n_keys is None else n_keys
+        code = np.zeros(n, np.int32)
+        seq = np.zeros(n, np.uint32)
+        _check(lib().cep_key_errors(self.h, query, code.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    seq.ctypes.data_as(C.POINTER(C.c_uint32)), n))
+        return code, seq
+
+    def digest(self, query: int = 0):
+        n, d = C.c_uint64(), C.c_uint64()
+        _check(lib().cep_match_digest(self.h, query, C.byref(n), C.byref(d)))
+        return n.value, d.value
+
+    def timing(self, query: int = 0):
+        ms, n = C.c_double(), C.c_uint32()
+        _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def watermark(self) -> int:
+        w = C.c_int64()
+        _check(lib().cep_watermark(self.h, C.byref(w)))
+        return w.value

@@ -1,0 +1,171 @@
+"""GPU parity: libcep.so's HIP kernels vs the CPU oracle and the reference's own KATs.
+
+Bit-exact on every array: match keys, emission events, walk pairs (stage, event) in
+reference order, per-key exception class and position, and the device checksum.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from fuzz_queries import random_query, random_stream
+from gpu_helpers import assert_parity, gpu_run
+from ref_queries import STOCK_KATS, STRING_KATS, build_case, kats, sequences
+from kafkastreams_cep_amd import native as N
+from kafkastreams_cep_amd import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+NFA_CASES = [n for n in kats() if n in STRING_KATS or n in STOCK_KATS]
+
+
+@pytest.mark.parametrize("force_nfa", [False, True])
+@pytest.mark.parametrize("name", NFA_CASES)
+def test_reference_kats_on_gpu(name, force_nfa):
+    case = kats()[name]
+    q, off, cols = build_case(name, case)
+    ir = q.to_ir()
+    g = gpu_run(ir, off, cols, force_nfa=force_nfa)
+    assert int(g["err_code"][0]) == 0
+    if "expected_count" in case:
+        assert g["n_matches"] == case["expected_count"]
+    else:
+        names = N.Query(ir).stage_names
+        g["pair_seq_or_pos"] = g["pair_pos"]
+        exp = [{k: sorted(v) for k, v in e.items()} for e in case["expected"]]
+        assert sequences(g, names) == exp
+    assert_parity(g, oracle.run(ir, off, cols), off)
+
+
+def test_strict_kat_uses_stencil():
+    q, off, cols = build_case("nfa_strict_one_run", kats()["nfa_strict_one_run"])
+    assert gpu_run(q.to_ir(), off, cols)["kind"] == N.CEP_KIND_STENCIL
+
+
+@pytest.mark.parametrize("force_nfa", [False, True])
+def test_cfg2_strict_abc_small(force_nfa):
+    cfg = W.SynthConfig("t", "abc", 300, 400, 0xCE90000 + 2)
+    off, cols = W.generate(cfg)
+    ir = W.strict_abc_query().to_ir()
+    assert_parity(gpu_run(ir, off, cols, force_nfa=force_nfa), oracle.run(ir, off, cols, threads=8), off)
+
+
+def test_stencil_many_short_keys():
+    """More key starts than a 4096-event tile holds keys: the LDS boundary table path."""
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 6, size=20000)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    v = rng.integers(0, 16, size=int(off[-1])).astype(np.int32)
+    ir = W.strict_abc_query().to_ir()
+    assert_parity(gpu_run(ir, off, [v]), oracle.run(ir, off, [v], threads=8), off)
+
+
+@pytest.mark.parametrize("variant", ["readme", "test", "demo"])
+def test_cfg3_stock_small(variant):
+    cfg = W.SynthConfig("t", "stock", 1500, 1000, 0xCE90000 + 3)
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 667)[:1500])
+    if variant == "demo":
+        cols = [c.astype(np.int64) for c in cols]
+    ir = W.stock_query(variant).to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    assert r["n_matches"] > 100
+    assert_parity(gpu_run(ir, off, cols), r, off)
+
+
+def test_cfg4_any_kleene_small():
+    cfg = W.SynthConfig("t", "stock", 400, 300, 0xCE90000 + 4)
+    off, cols = W.generate(cfg)
+    ir = W.any_kleene_query().to_ir()
+    assert_parity(gpu_run(ir, off, cols), oracle.run(ir, off, cols, threads=8), off)
+
+
+def test_cfg5_multi_query_session():
+    cfg = W.SynthConfig("t", "stock", 500, 600, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(8)]
+    s = N.Session(qs)
+    s.push(off, cols)
+    for i, q in enumerate(qs):
+        m = s.matches(i)
+        r = oracle.run(q.ir, off, cols, threads=8)
+        assert m["n_matches"] == r["n_matches"]
+        np.testing.assert_array_equal(m["pair_stage"], r["pair_stage"])
+        assert s.digest(i)[0] == r["n_matches"]
+
+
+@pytest.mark.parametrize("seed", range(0, 160))
+def test_fuzz_queries_vs_oracle(seed):
+    q = random_query(seed)
+    ir = q.to_ir()
+    if oracle.compile_check(ir):
+        pytest.skip("reference compile-time exception")
+    off, cols = random_stream(seed, 60, 14)
+    assert_parity(gpu_run(ir, off, cols), oracle.run(ir, off, cols), off)
+
+
+def test_edge_cases_empty_and_single():
+    ir = W.stock_query("readme").to_ir()
+    # no keys at all
+    off = np.zeros(1, np.uint64)
+    g = gpu_run(ir, off, [np.zeros(0, np.int32), np.zeros(0, np.int32)])
+    assert g["n_matches"] == 0
+    # keys with 0 and 1 events around a full README key
+    case = kats()["stock_readme"]
+    ev = np.array(case["events"], np.int32)
+    off = np.array([0, 0, 1, 1, 9, 9], np.uint64)
+    price = np.concatenate([[100], ev[:, 0]]).astype(np.int32)
+    vol = np.concatenate([[1500], ev[:, 1]]).astype(np.int32)
+    g = gpu_run(ir, off, [price, vol])
+    assert_parity(g, oracle.run(ir, off, [price, vol]), off)
+    assert g["n_matches"] == 4 and set(g["key"].tolist()) == {3}
+
+
+def test_error_parity_npe_illegal_state():
+    """zeroOrMore stock variant with state.get (no getOrElse): a dip before any take makes
+    the PROCEED walk miss its predecessor (H2, IllegalStateException); README variant on a
+    stream starting with a dip reads a null fold (NullPointerException)."""
+    S = W.stock_query("test").schema
+    from kafkastreams_cep_amd import QueryBuilder
+    q = (QueryBuilder(S).select().where(lambda k, v, ts, s: v.volume > 1000).fold("avg", lambda k, v, c: v.price).then()
+         .select().zeroOrMore().skipTillNextMatch().where(lambda k, v, ts, s: v.price > s.get("avg"))
+         .fold("avg", lambda k, v, c: (c + v.price) / 2).fold("volume", lambda k, v, c: v.volume).then()
+         .select().skipTillNextMatch().where(lambda k, v, ts, s: v.volume < 0.8 * s.getOrElse("volume", 5000)).build())
+    ir = q.to_ir()
+    price = np.array([100, 90, 95, 120, 80], np.int32)
+    vol = np.array([1500, 900, 100, 900, 100], np.int32)
+    off = np.array([0, 5], np.uint64)
+    r = oracle.run(ir, off, [price, vol])
+    assert r["err_code"][0] in (1, 2)
+    assert_parity(gpu_run(ir, off, [price, vol]), r, off)
+
+
+def test_synth_generator_matches_numpy():
+    for kind, cfg in (("stock", W.SynthConfig("t", "stock", 300, 200, 99, key_base=12345)),
+                      ("abc", W.SynthConfig("t", "abc", 50, 1000, 7))):
+        d = N.synth_stream(kind, cfg.seed, cfg.n_keys, cfg.mean_events, cfg.key_base)
+        off_g, cols_g = d.download()
+        off_h, cols_h = W.generate(cfg)
+        np.testing.assert_array_equal(off_g, off_h)
+        for a, b in zip(cols_g, cols_h):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_device_resident_batch_and_digest():
+    cfg = W.SynthConfig("t", "stock", 2000, 500, 0xCE90000 + 3)
+    d = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events)
+    q = N.Query(W.stock_query("readme").to_ir())
+    s = N.Session(q)
+    s.push_device(d)
+    n, dig = s.digest(0)
+    off, cols = d.download()
+    r = oracle.run(q.ir, off, cols, threads=8)
+    g = gpu_run(q.ir, off, cols)
+    assert n == r["n_matches"] and (n, dig) == g["digest"]
+
+
+def test_watermark():
+    q = N.Query(W.stock_query("readme").to_ir())
+    s = N.Session(q)
+    off = np.array([0, 3], np.uint64)
+    s.push(off, [np.array([1, 2, 3], np.int32), np.array([1, 2, 3], np.int32)], ts=np.array([5, 9, 7]))
+    assert s.watermark() == 9

@@ -1,0 +1,69 @@
+"""CPU-side checks of the C-ABI boundary (no GPU calls): libcep.so loads, exports every
+symbol include/cep.h declares, and its host query compiler agrees with the reference's
+StatesFactory rules (stage counts, kernel choice, compile-time exceptions)."""
+import os
+import re
+
+import pytest
+
+import oracle
+from kafkastreams_cep_amd import EventSchema, QueryBuilder
+from kafkastreams_cep_amd import native as N
+from kafkastreams_cep_amd import workloads as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "cep.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cep_[a-z_]+)\s*\(", src)))
+
+
+def test_header_exports_match_binding():
+    assert header_functions() == sorted(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    for name in header_functions():
+        assert hasattr(L, name), name
+
+
+def test_compile_kinds():
+    q = N.Query(W.stock_query("readme").to_ir())
+    assert q.kind == N.CEP_KIND_NFA
+    # $final, R2, R1 (loop), W1 (wrapper), R0
+    assert q.info.n_stages == 5 and q.info.n_patterns == 3 and q.info.n_states == 2
+    assert q.stage_names == ["0", "1", "2", "$final"]
+    q = N.Query(W.stock_query("test").to_ir())
+    assert q.kind == N.CEP_KIND_NFA and q.info.n_stages == 4
+    s = N.Query(W.strict_abc_query().to_ir())
+    assert s.kind == N.CEP_KIND_STENCIL and s.info.arity == 3
+
+
+def _pred(k, v, ts, s):
+    return v.price > 1
+
+
+def test_compile_errors_match_reference():
+    S = EventSchema({"price": "int"})
+    # pattern ending in a Kleene stage: StatesFactory.java:102-104 -> NullPointerException
+    q = QueryBuilder(S).select().where(_pred).then().select().oneOrMore().where(_pred).build()
+    ir = q.to_ir()
+    assert oracle.compile_check(ir) == 1
+    assert N.Query(ir).info.compile_error == 1
+    # a pattern without where(): Stage.java:159 -> IllegalArgumentException
+    p = QueryBuilder(S).select().where(_pred).then()
+    ir = p.to_ir()
+    assert oracle.compile_check(ir) == 4
+    assert N.Query(ir).info.compile_error == 4
+    with pytest.raises(N.CepError):
+        N.Session(N.Query(ir))
+
+
+def test_bad_ir_is_rejected():
+    with pytest.raises(N.CepError):
+        N.Query(b"CEPQ\x02\x00\x00\x00")
+    with pytest.raises(N.CepError):
+        N.Query(W.stock_query().to_ir() + b"\x00")
