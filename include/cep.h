@@ -172,9 +172,10 @@ int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* c
  * that multi-GPU runs reduce with min. */
 int cep_watermark(cep_session* s, int64_t* out);
 
-/* Device time of the last batch's matching kernels, per query, from HIP events recorded
- * on the session stream (ms), and the launch count. */
-int cep_last_timing(cep_session* s, int query, double* kernel_ms, uint32_t* launches);
+/* Device time of the last batch, per query, from HIP events recorded on the session
+ * stream (ms): the matching kernel launches (kernel_ms, `launches` of them: nfa_kernel incl.
+ * capacity retries, or stencil_kernel) and the setup/compaction kernels (aux_ms). */
+int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);
 
 const char* cep_last_error(void);
 int cep_alloc_pinned(size_t bytes, void** out);

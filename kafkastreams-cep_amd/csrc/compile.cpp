@@ -413,6 +413,10 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   std::vector<int> seen;
   for (auto& p : ps) {
     if (p.card != CARD_ONE || p.strat != STRICT || !total(p.pred.get())) stencil = false;
+    // folds never influence a stencil match, but they run on every BEGIN and can throw
+    // (a null `curr` unboxed, integer division): only total folds keep the stencil exact
+    for (auto& a : p.aggs)
+      if (!total(a.second.get())) stencil = false;
     for (int s : seen) if (s == p.name) stencil = false;
     seen.push_back(p.name);
   }

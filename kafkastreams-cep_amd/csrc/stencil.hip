@@ -229,10 +229,17 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
     } else {
       __hip_atomic_store(&A.status[t], (1ull << 62) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int64_t pp = (int64_t)t - 1;
+      uint32_t spins = 0;
       while (pp >= 0) {
         const unsigned long long s = __hip_atomic_load(&A.status[pp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long flag = s >> 62;
         if (flag == 0) {
+          // predecessors took their tickets earlier, so they are resident and will publish;
+          // the bound only turns a bug into a reported error instead of a hang
+          if (++spins > (1u << 24)) {
+            atomicOr(A.overflow, 2u);
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }

@@ -74,7 +74,8 @@ def lib():
             "cep_key_errors": ([vp, C.c_int, C.POINTER(i32), C.POINTER(u32), u64], C.c_int),
             "cep_match_digest": ([vp, C.c_int, C.POINTER(u64), C.POINTER(u64)], C.c_int),
             "cep_watermark": ([vp, C.POINTER(C.c_int64)], C.c_int),
-            "cep_last_timing": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(u32)], C.c_int),
+            "cep_last_timing": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u32)],
+                                C.c_int),
             "cep_last_error": ([], C.c_char_p),
             "cep_device_alloc": ([C.c_int, C.c_size_t, C.POINTER(vp)], C.c_int),
             "cep_device_free": ([vp], C.c_int),
@@ -272,9 +273,10 @@ class Session:
         return n.value, d.value
 
     def timing(self, query: int = 0):
-        ms, n = C.c_double(), C.c_uint32()
-        _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(n)))
-        return ms.value, n.value
+        """(matching-kernel ms, setup/compaction ms, matching launches) of the last batch."""
+        ms, aux, n = C.c_double(), C.c_double(), C.c_uint32()
+        _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(aux), C.byref(n)))
+        return ms.value, aux.value, n.value
 
     def watermark(self) -> int:
         w = C.c_int64()
