@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""bench.py — events/sec of the README stock Kleene+ query on 1/2/4/8 MI355X.
+
+BASELINE.json metric: "events/sec (whole node) + matches/sec, stock Kleene+ query, 1M keys,
+1/2/4/8 GPU".  One step = one pass of the matcher (libcep.so: nfa_kernel + compaction) over
+one batch of 1M keys x ~1000 events per GPU (config 3's shape), inputs already
+resident in HBM, every key starting from the NFA's initial state.  Keys are sharded across
+ranks with no data-path collective (weak scaling: each rank owns its own 1M keys); RCCL only
+all-gathers counts/checksums and reduces the watermark.
+
+    python bench.py                      # N=1, defaults finish in a few minutes
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (contract in the task statement; fields documented in
+DESIGN.md §7).  `roofline` prices nfa_kernel at SURVEY §8(d)'s algorithmic bytes (columns read
+once + 4 B per emitted event id + 4 B per match) against 8 TB/s; `cpu_baseline` times the
+oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/64 key
+sample on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import cepamd  # noqa: E402,F401
+from kafkastreams_cep_amd import native as N  # noqa: E402
+from kafkastreams_cep_amd import workloads as W  # noqa: E402
+
+METRIC = "events/sec (whole node) + matches/sec, stock Kleene+ query, 1M keys, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+class Dist:
+    """torch.distributed (nccl = RCCL over xGMI) when launched with WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl")
+            self.torch, self.dist = torch, dist
+
+    def barrier(self):
+        if self.torch:
+            self.dist.barrier()
+            self.torch.cuda.synchronize()
+
+    def gather(self, vals):
+        """all-gather a small float64 vector from every rank -> [world, len]"""
+        if not self.torch:
+            return np.asarray([vals], dtype=np.float64)
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.stack([o.cpu().numpy() for o in out])
+
+    def min_i64(self, v):
+        if not self.torch:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.int64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return int(t.item())
+
+    def close(self):
+        if self.torch:
+            self.dist.destroy_process_group()
+
+
+def run_steps(sess, stream, steps, warmup, dist):
+    for _ in range(warmup):
+        sess.push_device(stream)
+    kern, aux = [], []
+    dist.barrier()
+    N.lib().cep_sync(sess.h)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sess.push_device(stream)  # returns after the batch's kernels complete
+        k, a, _ = sess.timing(0)
+        kern.append(k)
+        aux.append(a)
+    N.lib().cep_sync(sess.h)
+    dist.barrier()
+    return time.perf_counter() - t0, float(np.mean(kern)), float(np.mean(aux))
+
+
+def load_traffic(name):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(cfg, variant, threads, every):
+    """Oracle on keys 0, every, 2*every, ... of the same stream (numpy generator = GPU
+    generator bit for bit).  Also checks GPU == oracle on that sample (checksum)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the checker / CPU baseline only
+
+    keys = np.arange(0, cfg.n_keys, every)
+    off, cols = W.generate(cfg, keys)
+    ir = W.stock_query(variant).to_ir()
+    r = oracle.run(ir, off, cols, threads=threads)
+    n_ev = int(off[-1])
+    # parity spot check on the sample: device checksum vs host checksum of the oracle output
+    emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+    pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+    pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+    want = (r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]))
+    s = N.Session(N.Query(ir), device=0)
+    s.push(off, cols)
+    got = s.digest(0)
+    s.close()
+    return {"value": n_ev / r["elapsed_s"], "unit": "events/s", "cores": r["threads"], "kind": "port",
+            "sample": f"{len(keys)} of {cfg.n_keys} keys (every {every}th), {n_ev} events, "
+                      f"{r['n_matches']} matches, {r['elapsed_s']:.2f} s on {r['threads']} threads",
+            "matches_per_s": r["n_matches"] / r["elapsed_s"],
+            "parity_on_sample": bool(got == want)}
+
+
+def secondary_strict(device, steps, warmup, dist):
+    """Config 2: strict SEQ(A,B,C), 1e8 events over 1e4 keys, stencil_kernel."""
+    cfg = W.CONFIGS[2]
+    stream = N.synth_stream("abc", cfg.seed, cfg.n_keys, cfg.mean_events, 0, device)
+    q = N.Query(W.strict_abc_query().to_ir())
+    s = N.Session(q, device=device)
+    el, kms, _ = run_steps(s, stream, steps, warmup, dist)
+    n_m, _ = s.digest(0)
+    n_ev = stream.n_events
+    alg = 4.0 * n_ev + 16.0 * n_m  # one int column + (key + 3 event ids) per match
+    res = {"workload": "cfg2: strict SEQ(A,B,C) v<4 | 4<=v<8 | v>=8, 1e4 keys x 1e4 events",
+           "value": n_ev * steps / el, "unit": "events/s", "matches_per_step": n_m,
+           "ms_per_step": 1e3 * el / steps,
+           "roofline": {"bound": "hbm", "achieved": alg / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "traffic": load_traffic("stencil_kernel"), "kernel": "stencil_kernel",
+                        "kernel_ms": kms, "algorithmic_bytes": alg}}
+    s.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--keys", type=int, default=1_000_000, help="keys per GPU")
+    ap.add_argument("--mean", type=int, default=1000, help="mean events per key")
+    ap.add_argument("--variant", default="readme", choices=["readme", "test"])
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-every", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    dist = Dist()
+    if dist.world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
+    device = dist.local
+    cfg = W.SynthConfig("cfg3_stock", "stock", args.keys, args.mean, W.CONFIGS[3].seed,
+                        key_base=dist.rank * args.keys)
+    stream = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events, cfg.key_base, device)
+    q = N.Query(W.stock_query(args.variant).to_ir())
+    sess = N.Session(q, device=device)
+    el, kms, aux_ms = run_steps(sess, stream, args.steps, args.warmup, dist)
+    n_m, digest = sess.digest(0)
+    code, _ = sess.key_errors(0)
+    n_err = int(np.count_nonzero(code))
+    # pairs emitted (event ids): from the flat output of the last step
+    m = N.Matches()
+    N._check(N.lib().cep_poll_matches(sess.h, 0, N.CEP_MEM_DEVICE, N.C.byref(m)))
+    n_pairs = m.n_pairs
+    wm = dist.min_i64(sess.watermark())
+    per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err), float(digest % (1 << 52))])
+    tot_ev, tot_m = per[:, 0].sum(), per[:, 1].sum()
+    t_max = per[:, 3].max()
+
+    if dist.rank == 0:
+        alg = 8.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m  # SURVEY §8(d), rank 0's launch
+        achieved = alg / (kms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": tot_ev * args.steps / t_max,
+            "unit": "events/s",
+            "matches_per_s": tot_m * args.steps / t_max,
+            "n_gpus": dist.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * t_max / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: SplitMix64 stock random walk (SURVEY §8d), generated in HBM",
+            "config": {"workload": f"cfg3 README stock query SEQ(Stock+ a[], Stock b) skip_till_next, "
+                                   f"folds avg/volume, WITHIN 1h ({args.variant} variant)",
+                       "keys_per_gpu": args.keys, "events_per_gpu": int(stream.n_events),
+                       "matches_per_gpu_step": int(n_m), "parallelism": f"key-sharded x{dist.world}",
+                       "key_errors": int(per[:, 5].sum())},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("nfa_kernel"),
+                         "kernel": "nfa_kernel", "kernel_ms": kms, "compaction_ms": aux_ms,
+                         "algorithmic_bytes": alg},
+            "watermark": wm,
+        }
+        if dist.world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.variant, args.cpu_threads, args.cpu_every)
+        if dist.world == 1 and not args.no_secondary:
+            out["secondary"] = secondary_strict(device, args.steps, args.warmup, dist)
+        print(json.dumps(out), flush=True)
+    sess.close()
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,10 +103,19 @@ int cep_query_info_get(const cep_query* q, cep_query_info* info);
 /* stage name of id `name_id` (UTF-8, NUL-terminated, owned by the query) */
 const char* cep_query_stage_name(const cep_query* q, uint32_t name_id);
 void cep_query_destroy(cep_query* q);
+/* The generated C++ of the query's NFA step (what CEP_TIER_JIT compiles), owned by the query. */
+const char* cep_query_jit_source(const cep_query* q);
+/* Compile the query's JIT kernel into the on-disk code-object cache without a GPU
+ * ($CEP_JIT_CACHE, default <libcep.so dir>/jit_cache); sessions then load it directly. */
+int cep_jit_precompile(const cep_query* q, double* compile_s);
+
+#define CEP_TIER_JIT 0     /* NFA queries run their own kernel, generated and compiled by hipRTC */
+#define CEP_TIER_INTERP 1  /* NFA queries run the precompiled bytecode-interpreter kernel */
 
 typedef struct {
   int device;             /* HIP device ordinal */
   int force_nfa;          /* 1: run CEP_KIND_STENCIL queries on the general NFA kernel */
+  int tier;               /* CEP_TIER_JIT (default) or CEP_TIER_INTERP */
   uint32_t max_runs;      /* live runs per key (0 = default 32); retried x8 on overflow */
   double pool_factor;     /* buffer pool size per event of the batch (0 = default) */
 } cep_opts;
@@ -132,8 +141,8 @@ typedef struct {
 } cep_batch;
 
 /* Runs every query of the session over the batch.  Each batch starts every key from the
- * NFA's initial state (one batch = one stream segment per key).  Asynchronous on the
- * session's stream; cep_sync / cep_poll_matches wait for it. */
+ * NFA's initial state (one batch = one stream segment per key).  Returns once the batch's
+ * kernels have completed (buffers are borrowed for the call only). */
 int cep_push_batch(cep_session* s, const cep_batch* b);
 int cep_sync(cep_session* s);
 

@@ -21,6 +21,7 @@ struct cep_query {
   int rangeCols[2] = {0, 0};
   int nRangeCols = 0;
   int64_t rangeLo[8][2]{}, rangeHi[8][2]{};
+  std::string jitSource;  // per-query NFA step policy for hipRTC (jit.cpp)
 };
 
 namespace cep {
@@ -47,5 +48,7 @@ hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_b
                         int32_t* c0, int32_t* c1, hipStream_t st);
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
 uint64_t synth_hash_host(uint64_t seed, uint64_t key, uint64_t j);
+std::vector<char> jit_code_object(const std::string& src, double* compile_s);
+std::string jit_cache_key(const std::string& src);
 
 }  // namespace cep

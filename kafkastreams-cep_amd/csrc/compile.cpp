@@ -309,6 +309,372 @@ struct Builder {
   }
 };
 
+
+// ============================================================ JIT source generation
+// Emits the per-query step policy compiled by hipRTC (jit.cpp): fields loaded once per
+// event into registers, predicates and folds as straight-line Java-semantics code, and one
+// function per stage implementing NFA.evaluate (nfa/NFA.java:162-250) with its edges,
+// targets and aggregates as constants; PROCEED edges become direct calls.
+namespace {
+
+const char* ctype(int t) { return t == 1 ? "int32_t" : t == 2 ? "int64_t" : t == 3 ? "double" : "bool"; }
+
+std::string lit(const Expr* e) {
+  char b[64];
+  switch (e->op) {
+    case 0x01: std::snprintf(b, sizeof b, "((int32_t)%d)", (int)e->i); break;
+    case 0x02: std::snprintf(b, sizeof b, "((int64_t)0x%llxull)", (unsigned long long)e->i); break;
+    case 0x03: {
+      uint64_t bits;
+      std::memcpy(&bits, &e->d, 8);
+      std::snprintf(b, sizeof b, "__longlong_as_double((long long)0x%llxull)", (unsigned long long)bits);
+      break;
+    }
+    default: std::snprintf(b, sizeof b, "%s", e->i ? "true" : "false"); break;
+  }
+  return b;
+}
+
+struct Gen {
+  std::string s;
+  int n = 0;
+  std::string fail;   // statement tail after `err = X;` (e.g. "return false;")
+  int aggType = 0;    // state type of `curr` inside an aggregator
+  std::string t() { return "t" + std::to_string(n++); }
+  void raise(const char* code, const std::string& cond) { s += "  if (" + cond + ") { err = " + code + "; " + fail + " }\n"; }
+
+  // returns (value, null-flag or "")
+  std::pair<std::string, std::string> expr(const Expr* e) {
+    switch (e->op) {
+      case 0x01: case 0x02: case 0x03: case 0x04: return {lit(e), ""};
+      case 0x05: return {"ev.f" + std::to_string(e->idx), ""};
+      case 0x06: return {"ev.ts", ""};
+      case 0x07: case 0x08: {
+        const std::string si = std::to_string(e->idx);
+        std::string dflt;
+        if (e->op == 0x08) dflt = operand(e->a.get());  // the default argument is evaluated first
+        const int st = stateType[e->idx];
+        const std::string v = t();
+        const std::string raw = st == 3 ? "__longlong_as_double(w.v[" + si + "])" : "(" + std::string(ctype(st)) + ")w.v[" + si + "]";
+        const std::string nul = "((w.nm >> " + si + ") & 1u)";
+        if (e->op == 0x08) {
+          s += "  const " + std::string(ctype(st)) + " " + v + " = " + nul + " ? " + dflt + " : " + raw + ";\n";
+          return {v, ""};
+        }
+        const std::string nf = t();
+        s += "  const " + std::string(ctype(st)) + " " + v + " = " + raw + ";\n";
+        s += "  const bool " + nf + " = " + nul + ";\n";
+        return {v, nf};
+      }
+      case 0x09: return {"curr", "curr_null"};
+      case 0x10: case 0x11: case 0x12: case 0x13: case 0x14: {
+        const std::string a = operand(e->a.get()), b = operand(e->b.get());
+        const std::string v = t();
+        const int ty = e->t;
+        std::string val;
+        if (ty == 3) {
+          static const char* fn[] = {"__dadd_rn", "__dsub_rn", "__dmul_rn", "__ddiv_rn", "fmod"};
+          val = std::string(fn[e->op - 0x10]) + "(" + a + ", " + b + ")";
+        } else {
+          const std::string U = ty == 1 ? "uint32_t" : "uint64_t", T = ctype(ty);
+          switch (e->op) {
+            case 0x10: val = "(" + T + ")((" + U + ")" + a + " + (" + U + ")" + b + ")"; break;
+            case 0x11: val = "(" + T + ")((" + U + ")" + a + " - (" + U + ")" + b + ")"; break;
+            case 0x12: val = "(" + T + ")((" + U + ")" + a + " * (" + U + ")" + b + ")"; break;
+            case 0x13:
+              raise("KE_ARITH", b + " == 0");
+              val = "(" + b + " == -1) ? (" + T + ")((" + U + ")0 - (" + U + ")" + a + ") : (" + T + ")(" + a + " / " + b + ")";
+              break;
+            default:
+              raise("KE_ARITH", b + " == 0");
+              val = "(" + b + " == -1) ? (" + T + ")0 : (" + T + ")(" + a + " % " + b + ")";
+              break;
+          }
+        }
+        s += "  const " + std::string(ctype(ty)) + " " + v + " = " + val + ";\n";
+        return {v, ""};
+      }
+      case 0x15: {
+        const std::string a = operand(e->a.get());
+        const std::string v = t();
+        std::string val = e->t == 3 ? "-" + a
+                        : e->t == 1 ? "(int32_t)(0u - (uint32_t)" + a + ")"
+                                    : "(int64_t)((uint64_t)0 - (uint64_t)" + a + ")";
+        s += "  const " + std::string(ctype(e->t)) + " " + v + " = " + val + ";\n";
+        return {v, ""};
+      }
+      case 0x18: {
+        const std::string a = operand(e->a.get());
+        const std::string v = t();
+        const int f = e->t2, to = e->t;
+        std::string val;
+        if (f == to) val = a;
+        else if (f == 3) val = to == 1 ? "(int32_t)java_d2i(" + a + ")" : "java_d2l(" + a + ")";
+        else if (to == 3) val = "(double)" + a;
+        else if (to == 1) val = "(int32_t)(uint32_t)(uint64_t)" + a;
+        else val = "(int64_t)" + a;
+        s += "  const " + std::string(ctype(to)) + " " + v + " = " + val + ";\n";
+        return {v, ""};
+      }
+      case 0x20: case 0x21: case 0x22: case 0x23: case 0x24: case 0x25: {
+        static const char* op[] = {"<", "<=", ">", ">=", "==", "!="};
+        const std::string a = operand(e->a.get()), b = operand(e->b.get());
+        const std::string v = t();
+        s += "  const bool " + v + " = " + a + " " + op[e->op - 0x20] + " " + b + ";\n";
+        return {v, ""};
+      }
+      case 0x30: case 0x31: {
+        const std::string v = t();
+        s += "  bool " + v + ";\n  {\n";
+        const std::string a = operand(e->a.get());
+        s += "  if (" + std::string(e->op == 0x30 ? "!" : "") + a + ") " + v + " = " + (e->op == 0x30 ? "false" : "true") + ";\n  else {\n";
+        const std::string b = operand(e->b.get());
+        s += "  " + v + " = " + b + ";\n  }\n  }\n";
+        return {v, ""};
+      }
+      case 0x32: {
+        const std::string a = operand(e->a.get());
+        const std::string v = t();
+        s += "  const bool " + v + " = !" + a + ";\n";
+        return {v, ""};
+      }
+    }
+    throw std::runtime_error("codegen: bad expression");
+  }
+  std::string operand(const Expr* e) {
+    auto r = expr(e);
+    if (!r.second.empty()) raise("KE_NPE", r.second);  // unboxing a null Integer/Long
+    return r.first;
+  }
+  std::string matcher(const M* m) {
+    switch (m->k) {
+      case M::TRUE_: return "true";
+      case M::LEAF: return operand(m->leaf);
+      case M::NOT: {
+        const std::string a = matcher(m->a.get());
+        const std::string v = t();
+        s += "  const bool " + v + " = !" + a + ";\n";
+        return v;
+      }
+      default: {
+        const std::string v = t();
+        s += "  bool " + v + ";\n  {\n";
+        const std::string a = matcher(m->a.get());
+        s += "  if (" + std::string(m->k == M::AND ? "!" : "") + a + ") " + v + " = " + (m->k == M::AND ? "false" : "true") + ";\n  else {\n";
+        const std::string b = matcher(m->b.get());
+        s += "  " + v + " = " + b + ";\n  }\n  }\n";
+        return v;
+      }
+    }
+  }
+  std::vector<int> stateType;
+};
+
+void uses(const Expr* e, std::vector<bool>& fields, bool& ts) {
+  if (!e) return;
+  if (e->op == 0x05) fields[e->idx] = true;
+  if (e->op == 0x06) ts = true;
+  uses(e->a.get(), fields, ts);
+  uses(e->b.get(), fields, ts);
+}
+void usesM(const M* m, std::vector<bool>& fields, bool& ts) {
+  if (!m) return;
+  if (m->k == M::LEAF) uses(m->leaf, fields, ts);
+  usesM(m->a.get(), fields, ts);
+  usesM(m->b.get(), fields, ts);
+}
+
+}  // namespace
+
+static std::string generate_jit(cep_query* q, Builder& b) {
+  const DevQuery& d = q->dev;
+  const int F = d.n_states <= 2 ? 2 : d.n_states <= 4 ? 4 : 8;
+  std::vector<int> stTypes(d.state_type, d.state_type + d.n_states);
+  std::vector<bool> fields(d.n_fields, false);
+  bool ts = false;
+  for (auto& pe : b.pending) usesM(pe.m.get(), fields, ts);
+  for (auto& sa : b.stageAggs)
+    for (auto& a : *sa.second) uses(a.second.get(), fields, ts);
+  std::string o;
+  o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
+  o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
+  o += "#include \"dewey.h\"\n#include \"java.h\"\n#include \"nfa_lane.h\"\n\nnamespace cep {\nnamespace {\n\n";
+  o += "constexpr int F = " + std::to_string(F) + ";\n";
+  o += "struct Ev {\n";
+  for (uint32_t f = 0; f < d.n_fields; f++)
+    if (fields[f]) o += "  " + std::string(ctype(d.field_type[f])) + " f" + std::to_string(f) + ";\n";
+  o += "  int64_t ts;\n};\n";
+  o += "struct Fo {\n  int64_t v[F];\n  uint32_t nm;\n};\n";
+  o += "struct Top {\n  uint32_t stage, event, ev_first;\n};\n";
+  o += "struct Out {\n  int produced;\n  Rec<F>* same;\n};\n\n";
+  o += "__device__ __forceinline__ void load_ev(Ev& ev, const NfaArgs& A, uint64_t pos) {\n";
+  for (uint32_t f = 0; f < d.n_fields; f++)
+    if (fields[f])
+      o += "  ev.f" + std::to_string(f) + " = ((const " + ctype(d.field_type[f]) + "*)A.cols.p[" + std::to_string(f) + "])[pos];\n";
+  o += ts ? "  ev.ts = A.ts ? A.ts[pos] : (int64_t)pos;\n" : "  ev.ts = 0;\n";
+  o += "}\n\n";
+  // predicates, one per (stage, edge); folds one per (stage, aggregate)
+  std::vector<std::vector<std::string>> predName(d.n_stages, std::vector<std::string>(3));
+  for (auto& pe : b.pending) {
+    if (pe.m->k == M::TRUE_) { predName[pe.stage][pe.edge] = ""; continue; }
+    Gen g;
+    g.stateType = stTypes;
+    g.fail = "return false;";
+    const std::string v = g.matcher(pe.m.get());
+    const std::string name = "P" + std::to_string(pe.stage) + "_" + std::to_string(pe.edge);
+    predName[pe.stage][pe.edge] = name;
+    o += "__device__ __forceinline__ bool " + name + "(const Ev& ev, const Fo& w, int& err) {\n" + g.s + "  return " + v + ";\n}\n";
+  }
+  std::vector<std::vector<std::string>> aggName(d.n_stages);
+  for (auto& sa : b.stageAggs) {
+    int k = 0;
+    for (auto& a : *sa.second) {
+      const int st = stTypes[a.first];
+      Gen g;
+      g.stateType = stTypes;
+      g.fail = "return;";
+      g.aggType = st;
+      const std::string si = std::to_string(a.first);
+      std::string head = "  const bool curr_null = (w.nm >> " + si + ") & 1u;\n";
+      head += st == 3 ? "  const double curr = __longlong_as_double(w.v[" + si + "]);\n"
+                      : "  const " + std::string(ctype(st)) + " curr = (" + ctype(st) + ")w.v[" + si + "];\n";
+      auto r = g.expr(a.second.get());
+      const std::string name = "A" + std::to_string(sa.first) + "_" + std::to_string(k++);
+      aggName[sa.first].push_back(name);
+      std::string store = st == 3 ? "__double_as_longlong(" + r.first + ")" : "(int64_t)" + r.first;
+      std::string nul = r.second.empty() ? "0u" : "(" + r.second + " ? 1u : 0u)";
+      o += "__device__ __forceinline__ void " + name + "(const Ev& ev, Fo& w, int& err) {\n" + head + g.s +
+           "  w.v[" + si + "] = " + store + ";\n  w.nm = (w.nm & ~(1u << " + si + ")) | (" + nul + " << " + si + ");\n}\n";
+    }
+  }
+  o += "\nstruct JitQ {\n  const NfaArgs& A;\n";
+  const DevStage& bs = d.st[d.begin_stage];
+  const bool quiet = bs.n_edges == 1 && bs.e[0].op == OP_BEGIN;
+  o += "  static constexpr bool quiet = " + std::string(quiet ? "true" : "false") + ";\n";
+  o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
+  o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
+  o += "  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {\n    if (sw & kRecEps) return (sw >> 8) & 0xFF;\n    switch (sw & 0xFF) {\n";
+  for (uint32_t s = 0; s < d.n_stages; s++) o += "      case " + std::to_string(s) + ": return " + std::to_string(d.st[s].sk) + ";\n";
+  o += "    }\n    return 0;\n  }\n";
+  o += "  __device__ __forceinline__ uint16_t sk_name(uint32_t sk) const {\n    switch (sk) {\n";
+  for (uint32_t k = 0; k < d.n_sk; k++) o += "      case " + std::to_string(k) + ": return " + std::to_string(d.sk_name[k]) + ";\n";
+  o += "    }\n    return 0;\n  }\n";
+  o += "  template <class LT>\n  __device__ __forceinline__ bool begin_pred(LT& L) {\n";
+  if (quiet && !predName[d.begin_stage][0].empty()) {
+    o += "    Ev ev;\n    load_ev(ev, A, L.base + L.j);\n    Fo w;\n    w.nm = (1u << F) - 1;\n    int err = 0;\n";
+    o += "    const bool r = " + predName[d.begin_stage][0] + "(ev, w, err);\n    if (err) L.err = err;\n    return r;\n";
+  } else {
+    o += "    return true;\n";
+  }
+  o += "  }\n";
+  // stage functions in reverse creation order so that PROCEED targets are declared first:
+  // targets always have a smaller stage index ($final = 0, built last -> first)
+  for (uint32_t s = 0; s < d.n_stages; s++) {
+    const DevStage& S = d.st[s];
+    if (S.type == ST_FINAL) continue;
+    const std::string SK = std::to_string(S.sk), SI = std::to_string(s);
+    std::string f;
+    f += "  template <class LT>\n  __device__ __forceinline__ void E" + SI +
+         "(LT& L, const Top& top, const Dewey& ver, bool branching, uint32_t prev_sk, const Ev& ev, Fo& w, Out& o) {\n";
+    f += "    int err = 0;\n";
+    for (int e = 0; e < S.n_edges; e++) {  // matchEdgesAndGet: every predicate first, in order
+      const std::string& pn = predName[s][e];
+      f += "    const bool m" + std::to_string(e) + " = " + (pn.empty() ? std::string("true") : pn + "(ev, w, err)") + ";\n";
+      if (!pn.empty()) f += "    if (err) { L.err = err; return; }\n";
+    }
+    std::string hasT = "false", hasP = "false", hasI = "false", hasB = "false";
+    for (int e = 0; e < S.n_edges; e++) {
+      const std::string m = "m" + std::to_string(e);
+      if (S.e[e].op == OP_TAKE) hasT = m;
+      if (S.e[e].op == OP_PROCEED) hasP = m;
+      if (S.e[e].op == OP_IGNORE) hasI = m;
+      if (S.e[e].op == OP_BEGIN) hasB = m;
+    }
+    f += "    const bool br = (" + hasP + " && " + hasT + ") || (" + hasI + " && " + hasT + ") || (" + hasI + " && " + hasB +
+         ") || (" + hasI + " && " + hasP + ");\n";
+    f += "    bool consumed = false, ignored = false;\n    (void)consumed; (void)ignored;\n";
+    for (int e = 0; e < S.n_edges; e++) {
+      const DevEdge& E = S.e[e];
+      const std::string m = "m" + std::to_string(e);
+      if (E.op == OP_TAKE) {
+        f += "    if (" + m + ") {\n      if (!br) {\n";
+        f += "        Rec<F>* r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver);\n";
+        f += "        if (!r) return;\n        o.same = r;\n        o.produced++;\n";
+        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      } else {\n";
+        f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
+        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2);\n      }\n";
+        f += "      if (L.err) return;\n      consumed = true;\n    }\n";
+      } else if (E.op == OP_BEGIN) {
+        const bool fin = d.st[E.target].type == ST_FINAL;
+        f += "    if (" + m + ") {\n      L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n";
+        f += "      Rec<F>* r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
+             (fin ? " | kRecFinal" : "") + ", L.j, CEP_NONE, ver);\n";
+        f += "      if (!r) return;\n      o.same = r;\n      o.produced++;\n      consumed = true;\n    }\n";
+      } else if (E.op == OP_IGNORE) {
+        f += "    if (" + m + ") {\n      if (!br) {\n";
+        f += "        Rec<F>* r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver);\n";
+        f += "        if (!r) return;\n        o.same = r;\n        o.produced++;\n      }\n      ignored = true;\n    }\n";
+      } else {  // PROCEED
+        const DevStage& T = d.st[E.target];
+        const std::string TI = std::to_string(E.target);
+        f += "    if (" + m + ") {\n";
+        if (T.sk != S.sk) {
+          f += "      if (!branching) {\n        Dewey v2 = ver;\n        if (!dw_add_stage(v2)) { L.err = KE_CAPACITY; return; }\n";
+          f += "        E" + TI + "(L, top, v2, false, " + SK + ", ev, w, o);\n      } else {\n";
+          f += "        E" + TI + "(L, top, ver, true, " + SK + ", ev, w, o);\n      }\n";
+        } else {
+          f += "      E" + TI + "(L, top, ver, branching, " + SK + ", ev, w, o);\n";
+        }
+        f += "      if (L.err) return;\n    }\n";
+      }
+    }
+    f += "    if (br) {\n      if (prev_sk == kNoSk) { L.err = KE_NPE; return; }\n";
+    f += "      Dewey v2 = ver;\n      if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
+    f += "      Rec<F>* r = L.push_rec(kRecEps | kRecBranch | (prev_sk << 8) | " + SI +
+         "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2);\n      if (!r) return;\n";
+    f += "      uint32_t nm = (1u << F) - 1;\n";
+    for (int a = 0; a < S.n_aggs; a++) {
+      const std::string si = std::to_string(S.agg_state[a]);
+      f += "      if (!((w.nm >> " + si + ") & 1u)) { r->fold[" + si + "] = w.v[" + si + "]; nm &= ~(1u << " + si + "); }\n";
+    }
+    f += "      r->nullmask = nm;\n      o.produced++;\n";
+    f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
+    if (S.n_aggs) {
+      f += "    if (consumed) {\n";
+      for (auto& an : aggName[s]) f += "      " + an + "(ev, w, err);\n      if (err) { L.err = err; return; }\n";
+      f += "    }\n";
+    }
+    f += "  }\n";
+    o += f;
+  }
+  // step: dispatch on the record's stage (epsilon -> its PROCEED target, real -> begin stage)
+  o += "  template <class LT>\n  __device__ __forceinline__ int step(LT& L, const Rec<F>& c) {\n";
+  o += "    Ev ev;\n    load_ev(ev, A, L.base + L.j);\n    Fo w;\n";
+  o += "    for (int s = 0; s < F; s++) w.v[s] = c.fold[s];\n    w.nm = c.nullmask;\n";
+  o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, nullptr};\n";
+  o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
+  o += "    if (c.stage & kRecEps) {\n      const uint32_t esk = (c.stage >> 8) & 0xFF;\n      switch (c.stage & 0xFF) {\n";
+  for (uint32_t s = 0; s < d.n_stages; s++) {
+    if (d.st[s].type == ST_FINAL) continue;
+    const std::string SI = std::to_string(s), SK = std::to_string(d.st[s].sk);
+    o += "        case " + SI + ":\n          if (esk != " + SK + "u && !brf) {\n            Dewey v2 = c.ver;\n";
+    o += "            if (!dw_add_stage(v2)) { L.err = KE_CAPACITY; return -1; }\n";
+    o += "            E" + SI + "(L, top, v2, false, esk, ev, w, o);\n          } else {\n";
+    o += "            E" + SI + "(L, top, c.ver, brf, esk, ev, w, o);\n          }\n          break;\n";
+  }
+  o += "        default: L.err = KE_CAPACITY; return -1;\n      }\n    } else {\n";
+  o += "      E" + std::to_string(d.begin_stage) + "(L, top, c.ver, brf, kNoSk, ev, w, o);\n    }\n";
+  o += "    if (L.err) return -1;\n";
+  o += "    if (o.same) {\n      for (int s = 0; s < F; s++) o.same->fold[s] = w.v[s];\n      o.same->nullmask = w.nm;\n    }\n";
+  o += "    if (!(c.stage & kRecEps)) {  // begin state re-added with a new run (NFA.java:148-157)\n";
+  o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = KE_CAPACITY; return -1; }\n";
+  o += "      Rec<F>* r = L.push_rec(c.stage & 0xFF, CEP_NONE, CEP_NONE, v);\n      if (!r) return -1;\n";
+  o += "      r->nullmask = (1u << F) - 1;\n      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
+  o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256) cep_nfa_jit(NfaArgs A) {\n";
+  o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n}  // namespace cep\n";
+  return o;
+}
+
 void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   In in{ir, ir + n};
   if (n < 8 || std::memcmp(ir, "CEPQ", 4) != 0) throw std::runtime_error("not a CEP query IR (magic)");
@@ -460,6 +826,7 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
     q->info.kind = CEP_KIND_NFA;
     q->info.arity = 0;
   }
+  q->jitSource = generate_jit(q, b);
 }
 
 }  // namespace cep

@@ -1,0 +1,146 @@
+// dewey.h — DeweyVersion as run-length encoded (value, count) pairs, plus pool allocation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cep_layout.h"
+#include "kernel_args.h"
+
+namespace cep {
+
+// ------------------------------------------------------------------ DeweyVersion (RLE)
+// nfa/DeweyVersion.java: addRun :51-56, addStage :84-86, isCompatible :62-82.
+// Versions are canonical run-length encodings (adjacent pairs differ in value).  Every
+// operation indexes the pair arrays with compile-time indices only (unrolled selects), so a
+// Dewey held in a local stays in registers instead of scratch.
+constexpr int P = kDeweyPairs;
+
+__device__ __forceinline__ void dw_init(Dewey& d, int32_t v) {
+  d.n = 1;
+  d.len = 1;
+  d.v[0] = v;
+  d.c[0] = 1;
+#pragma unroll
+  for (int k = 1; k < P; k++) {
+    d.v[k] = 0;
+    d.c[k] = 0;
+  }
+}
+
+__device__ __forceinline__ int32_t dw_last(const Dewey& d) {
+  int32_t r = d.v[0];
+#pragma unroll
+  for (int k = 1; k < P; k++)
+    if ((uint32_t)k == d.n - 1) r = d.v[k];
+  return r;
+}
+
+// last digit + 1; false when the RLE would need more than kDeweyPairs pairs
+__device__ __forceinline__ bool dw_add_run(Dewey& d) {
+  const uint32_t i = d.n - 1;
+  uint32_t ci = 0;
+  int32_t vi = 0, vprev = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((uint32_t)k == i) { ci = d.c[k]; vi = d.v[k]; }
+    if ((uint32_t)k + 1 == i) vprev = d.v[k];
+  }
+  if (ci == 1) {
+    const int32_t nv = vi + 1;
+    const bool merge = i > 0 && vprev == nv;  // keep the encoding canonical
+#pragma unroll
+    for (int k = 0; k < P; k++) {
+      if ((uint32_t)k == i) {
+        d.v[k] = merge ? 0 : nv;
+        d.c[k] = merge ? 0 : 1;
+      }
+      if (merge && (uint32_t)k + 1 == i) d.c[k] += 1;
+    }
+    if (merge) d.n--;
+    return true;
+  }
+  if (d.n >= (uint32_t)P) return false;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((uint32_t)k == i) d.c[k] = ci - 1;
+    if ((uint32_t)k == i + 1) {
+      d.v[k] = vi + 1;
+      d.c[k] = 1;
+    }
+  }
+  d.n++;
+  return true;
+}
+
+// append digit 0
+__device__ __forceinline__ bool dw_add_stage(Dewey& d) {
+  const uint32_t i = d.n - 1;
+  const int32_t vi = dw_last(d);
+  if (vi == 0) {
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if ((uint32_t)k == i) d.c[k] += 1;
+    d.len++;
+    return true;
+  }
+  if (d.n >= (uint32_t)P) return false;
+#pragma unroll
+  for (int k = 0; k < P; k++)
+    if ((uint32_t)k == i + 1) {
+      d.v[k] = 0;
+      d.c[k] = 1;
+    }
+  d.n++;
+  d.len++;
+  return true;
+}
+
+// this.isCompatible(that)  (a = this, b = that)
+__device__ __forceinline__ bool dw_compatible(const Dewey& a, const Dewey& b) {
+  if (a.len > b.len) {
+    // b is a prefix of a: b's pairs but the last equal a's, b's last run is a prefix of a's run
+    if (b.n > a.n) return false;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < P; k++) {
+      if ((uint32_t)k + 1 < b.n) ok = ok && a.v[k] == b.v[k] && a.c[k] == b.c[k];
+      if ((uint32_t)k + 1 == b.n) ok = ok && a.v[k] == b.v[k] && a.c[k] >= b.c[k];
+    }
+    return ok;
+  }
+  if (a.len != b.len) return false;
+  // equal length: all digits but the last equal, then a.last >= b.last.  Dropping the last
+  // digit of a canonical RLE keeps it canonical: compare the shortened encodings exactly.
+  const uint32_t an = a.n, bn = b.n;
+  uint32_t alc = 0, blc = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((uint32_t)k + 1 == an) alc = a.c[k];
+    if ((uint32_t)k + 1 == bn) blc = b.c[k];
+  }
+  const uint32_t an2 = alc == 1 ? an - 1 : an, bn2 = blc == 1 ? bn - 1 : bn;
+  if (an2 != bn2) return false;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((uint32_t)k < an2) {
+      const uint32_t ca = a.c[k] - ((uint32_t)k + 1 == an ? 1u : 0u);
+      const uint32_t cb = b.c[k] - ((uint32_t)k + 1 == bn ? 1u : 0u);
+      ok = ok && a.v[k] == b.v[k] && ca == cb;
+    }
+  }
+  return ok && dw_last(a) >= dw_last(b);
+}
+
+// ------------------------------------------------------------------ pool allocation
+__device__ __forceinline__ uint32_t pool_take(const Pool& p, uint32_t& cur, uint32_t& end) {
+  if (cur == end) {
+    const uint32_t b = atomicAdd(p.top, p.chunk);
+    if (b >= p.cap || p.cap - b < p.chunk) return CEP_NONE;
+    cur = b;
+    end = b + p.chunk;
+  }
+  return cur++;
+}
+
+}  // namespace cep

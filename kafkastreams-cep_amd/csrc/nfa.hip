@@ -22,211 +22,48 @@
 
 #include "cep_layout.h"
 #include "nfa_device.h"
+#include "nfa_lane.h"
 
 namespace cep {
 
-constexpr uint32_t kNoSk = 0xFF;
-
+// Bytecode-interpreter policy (AOT tier): walks the DevQuery stage table and evaluates the
+// predicate/aggregate programs with interp().  NFA.evaluate's recursion over PROCEED edges
+// (nfa/NFA.java:162-250) is unrolled into a level stack: edges in order on the way down,
+// branch records and folds on the way back up (the recursion's return order).
 template <int F>
-struct Lane {
-  const NfaArgs& A;
+struct InterpQ {
   const DevQuery& q;
   const uint32_t* code;
-  // key
-  uint32_t key;
-  uint64_t base;
-  uint32_t j;  // current event (sequence number within key)
-  Rec<F>* ring;
-  uint32_t head = 0, count = 0;
-  // pools
-  uint32_t ncur = 0, nend = 0, pcur = 0, pend = 0;
-  uint32_t ochunk = CEP_NONE, opos = 0;
-  uint32_t cur_first = CEP_NONE;  // node chain of event j
-  int err = KE_OK;
-  uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
+  const NfaArgs& A;
+  bool quiet;
+  uint32_t begin_stage;
 
-  __device__ Lane(const NfaArgs& a, const DevQuery& qq, const uint32_t* c) : A(a), q(qq), code(c) {}
-
-  __device__ __forceinline__ Rec<F>& R(uint32_t i) { return ring[i % A.rcap]; }
-
-  // ---------------------------------------------------------------- buffer nodes
-  __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
-    for (uint32_t i = first; i != CEP_NONE;) {
-      const Node& n = A.nodes[i];
-      if ((n.meta & 0xFF) == sk) return (n.meta & 0x100) ? i : CEP_NONE;
-      i = n.same_next;
-    }
-    return CEP_NONE;
+  __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {
+    begin_stage = q.begin_stage;
+    const DevStage& b = q.st[begin_stage];
+    quiet = b.n_edges == 1 && b.e[0].op == OP_BEGIN;
   }
-
-  __device__ uint32_t new_node(uint32_t sk) {
-    const uint32_t i = pool_take(A.node_pool, ncur, nend);
-    if (i == CEP_NONE) { err = KE_CAPACITY; return CEP_NONE; }
-    Node& n = A.nodes[i];
-    n.event = j;
-    n.refs = 1;
-    n.head = n.tail = CEP_NONE;
-    n.same_next = cur_first;
-    n.meta = sk | 0x100;
-    cur_first = i;
-    return i;
-  }
-
-  __device__ void append_pred(uint32_t node, uint32_t prev, const Dewey& v) {
-    const uint32_t p = pool_take(A.pred_pool, pcur, pend);
-    if (p == CEP_NONE) { err = KE_CAPACITY; return; }
-    Pred& e = A.preds[p];
-    e.prev = prev;
-    e.next = CEP_NONE;
-    e.removed = 0;
-    e.ver = v;
-    Node& n = A.nodes[node];
-    if (n.head == CEP_NONE) n.head = p;
-    else A.preds[n.tail].next = p;
-    n.tail = p;
-    n.meta += 1u << 16;
-  }
-
-  // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
-  __device__ void put_begin(uint32_t sk, const Dewey& v) {
-    uint32_t c = lookup(sk, cur_first);
-    if (c == CEP_NONE) {
-      c = new_node(sk);
-      if (err) return;
-    } else {
-      Node& n = A.nodes[c];
-      n.refs = 1;
-      n.head = n.tail = CEP_NONE;
-      n.meta = sk | 0x100;
-    }
-    append_pred(c, CEP_NONE, v);
-  }
-
-  // put(curr, currEvent, prev, prevEvent, version)  :80-97
-  __device__ void put_link(uint32_t sk, uint32_t prev_sk, uint32_t prev_ev, uint32_t prev_first,
-                           const Dewey& v) {
-    if (prev_sk == kNoSk) { put_begin(sk, v); return; }
-    if (prev_ev == CEP_NONE) { err = KE_NPE; return; }
-    const uint32_t p = lookup(prev_sk, prev_first);
-    if (p == CEP_NONE) { err = KE_ILLEGAL_STATE; return; }
-    uint32_t c = lookup(sk, cur_first);
-    if (c == CEP_NONE) {
-      c = new_node(sk);
-      if (err) return;
-    }
-    append_pred(c, p, v);
-  }
-
-  // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92
-  __device__ __forceinline__ uint32_t first_compat(uint32_t node, const Dewey& walker) {
-    for (uint32_t p = A.nodes[node].head; p != CEP_NONE; p = A.preds[p].next) {
-      const Pred& e = A.preds[p];
-      if (e.removed) continue;
-      if (dw_compatible(walker, e.ver)) return p;
-    }
-    return CEP_NONE;
-  }
-
-  // branch  :99-110
-  __device__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v) {
-    if (ev == CEP_NONE) { err = KE_NPE; return; }
-    uint32_t s = lookup(sk, first);
-    Dewey w = v;
-    for (;;) {
-      if (s == CEP_NONE || !(A.nodes[s].meta & 0x100)) { err = KE_NPE; return; }
-      A.nodes[s].refs += 1;
-      const uint32_t p = first_compat(s, w);
-      if (p == CEP_NONE) return;
-      const uint32_t nx = A.preds[p].prev;
-      if (nx == CEP_NONE) return;
-      w = A.preds[p].ver;
-      s = nx;
-    }
-  }
-
-  // ---------------------------------------------------------------- output stream
-  __device__ __forceinline__ uint32_t out_slot() {  // global word index of the next word
-    if (ochunk == CEP_NONE || opos == kOutChunkWords - 1) {
-      const uint32_t c = atomicAdd(A.out_pool.top, 1u);
-      if (c >= A.out_pool.cap) { err = KE_CAPACITY; return CEP_NONE; }
-      if (ochunk == CEP_NONE) out_first = c;
-      else A.out[(uint64_t)ochunk * kOutChunkWords + kOutChunkWords - 1] = c;
-      ochunk = c;
-      opos = 0;
-    }
-    return (uint32_t)0;  // unused
-  }
-  __device__ __forceinline__ uint64_t out_put(uint32_t w) {
-    out_slot();
-    if (err) return 0;
-    const uint64_t a = (uint64_t)ochunk * kOutChunkWords + opos++;
-    A.out[a] = w;
-    return a;
-  }
-
-  // peek(stage, event, version, remove=true)  :143-171; emit = match construction
-  __device__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit) {
-    if (ev == CEP_NONE) { err = KE_NPE; return; }
-    uint32_t s = lookup(sk, first);
-    Dewey w = v;
-    uint64_t npair_addr = 0;
-    uint32_t np = 0;
-    if (emit) {
-      out_put(j);
-      npair_addr = out_put(0);
-      if (err) return;
-    }
-    for (;;) {
-      if (s == CEP_NONE) { err = KE_NPE; return; }
-      Node& n = A.nodes[s];
-      const uint32_t meta = n.meta;
-      if (!(meta & 0x100)) { err = KE_NPE; return; }
-      const int32_t left = n.refs == 0 ? 0 : n.refs - 1;
-      n.refs = left;
-      uint32_t live_preds = meta >> 16;
-      if (left == 0 && live_preds <= 1) n.meta = meta & ~0x100u;  // store.delete
-      if (emit) {
-        out_put(n.event);
-        out_put(q.sk_name[meta & 0xFF]);
-        np++;
-        if (err) return;
-      }
-      const uint32_t p = first_compat(s, w);
-      if (p == CEP_NONE) break;
-      if (left == 0) {  // removePredecessor(pointer)
-        A.preds[p].removed = 1;
-        n.meta -= 1u << 16;
-      }
-      const uint32_t nx = A.preds[p].prev;
-      if (nx == CEP_NONE) break;
-      w = A.preds[p].ver;
-      s = nx;
-    }
-    if (emit) {
-      A.out[npair_addr] = np;
-      n_matches++;
-      n_pairs += np;
-    }
-  }
-
-  // ---------------------------------------------------------------- records
   __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {
     return (sw & kRecEps) ? ((sw >> 8) & 0xFF) : q.st[sw & 0xFF].sk;
   }
-  __device__ __forceinline__ bool rec_is_final(uint32_t sw) const {
-    return (sw & kRecEps) && q.st[sw & 0xFF].type == ST_FINAL;
+  __device__ __forceinline__ uint16_t sk_name(uint32_t sk) const { return q.sk_name[sk]; }
+
+  template <class LaneT>
+  __device__ bool begin_pred(LaneT& lane) {
+    const DevEdge E = q.st[begin_stage].e[0];
+    if (E.prog == kProgTrue) return true;
+    int64_t W[F];
+    EvalIn in{&A.cols, q.field_type, A.ts, lane.base + lane.j, W, (1u << F) - 1, 0, true};
+    bool rn;
+    int ee = 0;
+    const int64_t r = interp(code, E.prog, in, &rn, &ee);
+    if (ee) lane.err = ee;
+    return r != 0;
   }
 
-  __device__ Rec<F>* push_rec() {
-    if (count >= A.rcap) { err = KE_CAPACITY; return nullptr; }
-    Rec<F>* r = &R(head + count);
-    count++;
-    return r;
-  }
-
-  // ---------------------------------------------------------------- one run step
-  // Returns the number of records produced; -1 on error.  `c` was popped from the ring.
-  __device__ int step(const Rec<F>& c) {
+  // NFA.matchPattern(ctx) :139-160.  Returns the number of records produced; -1 on error.
+  template <class LaneT>
+  __device__ int step(LaneT& lane, const Rec<F>& c) {
     int64_t W[F];
 #pragma unroll
     for (int s = 0; s < F; s++) W[s] = c.fold[s];
@@ -234,10 +71,10 @@ struct Lane {
     const uint32_t top = c.stage;
     const bool top_eps = top & kRecEps;
     const uint32_t top_sk = stage_sk(top);
+    const uint32_t j = lane.j;
     int produced = 0;
     Rec<F>* same_seq = nullptr;  // the (single) output record that keeps this run's sequence id
 
-    // level stack: cur stage, prev stage key, zeros appended, flags
     uint8_t lv_cur[kMaxStages + 1];
     uint8_t lv_prev[kMaxStages + 1];
     uint8_t lv_zeros[kMaxStages + 1];
@@ -248,15 +85,7 @@ struct Lane {
     lv_zeros[0] = 0;
     lv_flags[0] = (top & kRecBranch) ? 1 : 0;
 
-    EvalIn in;
-    in.cols = &A.cols;
-    in.ftype = q.field_type;
-    in.ts = A.ts;
-    in.pos = base + j;
-    in.W = W;
-    in.wnull = wnull;
-    in.curr = 0;
-    in.curr_null = true;
+    EvalIn in{&A.cols, q.field_type, A.ts, lane.base + j, W, wnull, 0, true};
 
     for (;;) {
       const bool eps = (L == 0) && top_eps;
@@ -264,7 +93,7 @@ struct Lane {
       const uint32_t cur_sk = eps ? top_sk : q.st[cur].sk;
       Dewey ver = c.ver;
       for (int z = 0; z < lv_zeros[L]; z++)
-        if (!dw_add_stage(ver)) { err = KE_CAPACITY; return -1; }
+        if (!dw_add_stage(ver)) { lane.err = KE_CAPACITY; return -1; }
       uint32_t proceed_target = CEP_NONE;
       if (eps) {
         proceed_target = cur;  // epsilon: single PROCEED(true) -> target (Stage.java:42-46)
@@ -277,7 +106,7 @@ struct Lane {
             bool rn;
             int ee = 0;
             const int64_t r = interp(code, S.e[e].prog, in, &rn, &ee);
-            if (ee) { err = ee; return -1; }
+            if (ee) { lane.err = ee; return -1; }
             hit = r != 0;
           }
           if (hit) matched |= 1u << e;
@@ -295,45 +124,34 @@ struct Lane {
           if (E.op == OP_PROCEED) {
             proceed_target = E.target;
           } else if (E.op == OP_TAKE) {
-            if (!br) {
-              Rec<F>* r = push_rec();
+            if (!br) {  // newEpsilonState(current, current), same run
+              Rec<F>* r = lane.push_rec(kRecEps | (cur_sk << 8) | cur, j, CEP_NONE, ver);
               if (!r) return -1;
-              r->stage = kRecEps | (cur_sk << 8) | cur;  // newEpsilonState(current, current)
-              r->event = j;
-              r->ev_first = CEP_NONE;
-              r->ver = ver;
               same_seq = r;
               produced++;
-              put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
+              lane.put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
             } else {
               Dewey v2 = ver;
-              if (!dw_add_run(v2)) { err = KE_CAPACITY; return -1; }
-              put_link(cur_sk, lv_prev[L], c.event, c.ev_first, v2);
+              if (!dw_add_run(v2)) { lane.err = KE_CAPACITY; return -1; }
+              lane.put_link(cur_sk, lv_prev[L], c.event, c.ev_first, v2);
             }
-            if (err) return -1;
+            if (lane.err) return -1;
             lv_flags[L] |= 4;
           } else if (E.op == OP_BEGIN) {
-            put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
-            if (err) return -1;
-            Rec<F>* r = push_rec();
-            if (!r) return -1;
+            lane.put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
+            if (lane.err) return -1;
             uint32_t sw = kRecEps | (cur_sk << 8) | E.target;
             if (q.st[E.target].type == ST_FINAL) sw |= kRecFinal;
-            r->stage = sw;
-            r->event = j;
-            r->ev_first = CEP_NONE;
-            r->ver = ver;
+            Rec<F>* r = lane.push_rec(sw, j, CEP_NONE, ver);
+            if (!r) return -1;
             same_seq = r;
             produced++;
             lv_flags[L] |= 4;
-          } else {  // IGNORE
-            if (!br) {  // re-add the context record (top stage/event, this level's version)
-              Rec<F>* r = push_rec();
+          } else {  // IGNORE: re-add the context record (top stage/event, this level's version)
+            if (!br) {
+              Rec<F>* r = lane.push_rec((top & ~(kRecBranch | kRecFinal)) | ((lv_flags[L] & 1) ? kRecBranch : 0),
+                                        c.event, c.ev_first, ver);
               if (!r) return -1;
-              r->stage = (top & ~(kRecBranch | kRecFinal)) | ((lv_flags[L] & 1) ? kRecBranch : 0);
-              r->event = c.event;
-              r->ev_first = c.ev_first;
-              r->ver = ver;
               same_seq = r;
               produced++;
             }
@@ -346,7 +164,7 @@ struct Lane {
       const uint32_t tsk = q.st[proceed_target].sk;
       const bool branching = lv_flags[L] & 1;
       const bool add = (tsk != cur_sk) && !branching;
-      if (L + 1 > kMaxStages) { err = KE_CAPACITY; return -1; }
+      if (L + 1 > kMaxStages) { lane.err = KE_CAPACITY; return -1; }
       lv_cur[L + 1] = (uint8_t)proceed_target;
       lv_prev[L + 1] = (uint8_t)cur_sk;
       lv_zeros[L + 1] = lv_zeros[L] + (add ? 1 : 0);
@@ -363,20 +181,14 @@ struct Lane {
       Dewey ver = c.ver;
       for (int z = 0; z < lv_zeros[l]; z++) dw_add_stage(ver);
       if (fl & 2) {  // isBranching :231-246
-        if (lv_prev[l] == kNoSk) { err = KE_NPE; return -1; }  // newEpsilonState(null, ...)
-        Rec<F>* r = push_rec();
-        if (!r) return -1;
-        r->stage = kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur;
-        if (fl & 8) {
-          r->event = c.event;
-          r->ev_first = c.ev_first;
-        } else {
-          r->event = j;
-          r->ev_first = CEP_NONE;
-        }
+        if (lv_prev[l] == kNoSk) { lane.err = KE_NPE; return -1; }  // newEpsilonState(null, ...)
         Dewey v2 = ver;
-        if (!dw_add_run(v2)) { err = KE_CAPACITY; return -1; }
-        r->ver = v2;
+        if (!dw_add_run(v2)) { lane.err = KE_CAPACITY; return -1; }
+        Rec<F>* r = (fl & 8) ? lane.push_rec(kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur, c.event,
+                                             c.ev_first, v2)
+                             : lane.push_rec(kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur, j,
+                                             CEP_NONE, v2);
+        if (!r) return -1;
         uint32_t nm = (1u << F) - 1;  // fresh sequence: only this stage's aggregates are copied
         for (int a = 0; a < S.n_aggs; a++) {
           const uint32_t s = S.agg_state[a];
@@ -387,8 +199,8 @@ struct Lane {
         }
         r->nullmask = nm;
         produced++;
-        walk_branch(lv_prev[l], c.event, c.ev_first, ver);
-        if (err) return -1;
+        lane.walk_branch(lv_prev[l], c.event, c.ev_first, ver);
+        if (lane.err) return -1;
       }
       if (fl & 4) {  // evaluateAggregates :259-265, declaration order
         for (int a = 0; a < S.n_aggs; a++) {
@@ -398,7 +210,7 @@ struct Lane {
           bool rn;
           int ee = 0;
           const int64_t v = interp(code, S.agg_prog[a], in, &rn, &ee);
-          if (ee) { err = ee; return -1; }
+          if (ee) { lane.err = ee; return -1; }
           W[s] = v;
           wnull = rn ? (wnull | (1u << s)) : (wnull & ~(1u << s));
         }
@@ -410,57 +222,14 @@ struct Lane {
     }
     // begin state re-added with a new run (:148-157)
     if (!top_eps && q.st[top & 0xFF].type == ST_BEGIN) {
-      Rec<F>* r = push_rec();
+      Dewey v = c.ver;
+      if (produced > 0 && !dw_add_run(v)) { lane.err = KE_CAPACITY; return -1; }
+      Rec<F>* r = lane.push_rec(top & 0xFF, CEP_NONE, CEP_NONE, v);
       if (!r) return -1;
-      r->stage = top & 0xFF;
-      r->event = CEP_NONE;
-      r->ev_first = CEP_NONE;
-      r->ver = c.ver;
-      if (produced > 0 && !dw_add_run(r->ver)) { err = KE_CAPACITY; return -1; }
       r->nullmask = (1u << F) - 1;
       produced++;
     }
     return produced;
-  }
-
-  // ---------------------------------------------------------------- one event
-  __device__ void event() {
-    cur_first = CEP_NONE;
-    const uint32_t n = count;
-    for (uint32_t i = 0; i < n; i++) {
-      const Rec<F> c = R(head);
-      head++;
-      count--;
-      const int produced = step(c);
-      if (err) return;
-      if (produced == 0) {  // removePattern
-        walk_remove(stage_sk(c.stage), c.event, c.ev_first, c.ver, false);
-        if (err) return;
-      }
-    }
-    // records created at this event learn the node chain of the event
-    for (uint32_t i = 0; i < count; i++) {
-      Rec<F>& r = R(head + i);
-      if (r.event == j) r.ev_first = cur_first;
-    }
-    // matchConstruction: finals in order, then drop them from the queue
-    bool any_final = false;
-    for (uint32_t i = 0; i < count; i++)
-      if (R(head + i).stage & kRecFinal) any_final = true;
-    if (!any_final) return;
-    const uint32_t m0 = n_matches, p0 = n_pairs;
-    uint32_t w = 0;
-    for (uint32_t i = 0; i < count; i++) {
-      const Rec<F> r = R(head + i);
-      if (r.stage & kRecFinal) {
-        walk_remove(stage_sk(r.stage), r.event, r.ev_first, r.ver, true);
-        if (err) { n_matches = m0; n_pairs = p0; return; }  // nothing of this event is forwarded
-      } else {
-        if (w != i) R(head + w) = r;
-        w++;
-      }
-    }
-    count = w;
   }
 };
 
@@ -477,44 +246,8 @@ __global__ void __launch_bounds__(256) nfa_kernel(NfaArgs A) {
   const uint32_t code_len = qs->code_len;
   for (uint32_t i = threadIdx.x; i < code_len; i += blockDim.x) code_s[i] = A.code[i];
   __syncthreads();
-
-  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nslots = A.key_list ? A.n_list : A.n_keys;
-  if (slot >= nslots) return;
-  const uint32_t key = A.key_list ? A.key_list[slot] : (uint32_t)slot;
-
-  Lane<F> L(A, *qs, code_s);
-  L.key = key;
-  L.base = A.key_off[key];
-  const uint32_t n = (uint32_t)(A.key_off[key + 1] - L.base);
-  L.ring = reinterpret_cast<Rec<F>*>(A.rings) + slot * A.rcap;
-  // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
-  {
-    Rec<F>& r = L.ring[0];
-    r.stage = qs->begin_stage;
-    r.event = CEP_NONE;
-    r.ev_first = CEP_NONE;
-    r.nullmask = (1u << F) - 1;
-    dw_init(r.ver, 1);
-    L.head = 0;
-    L.count = 1;
-  }
-  uint32_t err_seq = 0;
-  for (uint32_t j = 0; j < n; j++) {
-    L.j = j;
-    L.event();
-    if (L.err) {
-      err_seq = j;
-      break;
-    }
-  }
-  KeyState& ks = A.ks[key];
-  ks.n_matches = L.n_matches;
-  ks.n_pairs = L.n_pairs;
-  ks.out_first = L.out_first;
-  ks.err = L.err;
-  ks.err_seq = err_seq;
-  if (L.err == KE_CAPACITY) atomicAdd(A.n_capacity_err, 1u);
+  InterpQ<F> q(*qs, code_s, A);
+  run_key<F>(A, q);
 }
 
 // ---------------------------------------------------------------- compaction

@@ -78,6 +78,12 @@ struct QueryRt {
   const cep_query* q;
   int F = 2;
   DBuf d_q, d_code;
+  hipModule_t mod = nullptr;  // JIT tier: the query's own nfa kernel (cep_nfa_jit)
+  hipFunction_t fn = nullptr;
+  double jit_compile_s = 0;
+  ~QueryRt() {
+    if (mod) (void)hipModuleUnload(mod);
+  }
   // results of the last batch (device)
   DBuf m_key, m_emit, m_off, p_seq, p_stage;
   DBuf ks;
@@ -198,6 +204,14 @@ void run_stencil(cep_session* s, QueryRt& r) {
   HIPCHECK(hipStreamSynchronize(s->stream));
 }
 
+hipError_t launch_nfa_tier(QueryRt& r, NfaArgs& a, uint64_t nslots, hipStream_t st) {
+  if (!r.fn) return launch_nfa(r.F, a, nslots, r.q->dev.code_len, st);
+  if (nslots == 0) return hipSuccess;
+  size_t size = sizeof(NfaArgs);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  return hipModuleLaunchKernel(r.fn, (uint32_t)((nslots + 255) / 256), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
 void run_nfa(cep_session* s, QueryRt& r) {
   const cep_query* q = r.q;
   const uint64_t nk = s->n_keys;
@@ -245,7 +259,7 @@ void run_nfa(cep_session* s, QueryRt& r) {
   float total_ms = 0;
   r.launches = 0;
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
-  HIPCHECK(launch_nfa(r.F, a, nk, q->dev.code_len, s->stream));
+  HIPCHECK(launch_nfa_tier(r, a, nk, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   r.launches++;
   Scratch h{};
@@ -300,7 +314,7 @@ void run_nfa(cep_session* s, QueryRt& r) {
     a.key_list = s->keylist.as<uint32_t>();
     a.n_list = (uint32_t)list.size();
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
-    HIPCHECK(launch_nfa(r.F, a, list.size(), q->dev.code_len, s->stream));
+    HIPCHECK(launch_nfa_tier(r, a, list.size(), s->stream));
     HIPCHECK(hipEventRecord(s->ev1, s->stream));
     r.launches++;
     HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
@@ -385,6 +399,18 @@ const char* cep_query_stage_name(const cep_query* q, uint32_t id) {
 
 void cep_query_destroy(cep_query* q) { delete q; }
 
+const char* cep_query_jit_source(const cep_query* q) { return q ? q->jitSource.c_str() : nullptr; }
+
+int cep_jit_precompile(const cep_query* q, double* compile_s) {
+  if (!q) return fail(CEP_E_INVALID, "null query");
+  try {
+    jit_code_object(q->jitSource, compile_s);
+  } catch (std::exception& e) {
+    return fail(CEP_E_COMPILE, e.what());
+  }
+  return CEP_OK;
+}
+
 int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts, cep_session** out) {
   if (!queries || n_queries <= 0 || !out) return fail(CEP_E_INVALID, "need at least one query");
   for (int i = 0; i < n_queries; i++) {
@@ -414,6 +440,12 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
       r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());
       HIPCHECK(hipMemcpy(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
                          hipMemcpyHostToDevice));
+      const bool nfa = queries[i]->info.kind == CEP_KIND_NFA || s->opts.force_nfa;
+      if (nfa && s->opts.tier == CEP_TIER_JIT) {  // the query's own kernel, compiled by hipRTC
+        std::vector<char> co = jit_code_object(queries[i]->jitSource, &r->jit_compile_s);
+        HIPCHECK(hipModuleLoadData(&r->mod, co.data()));
+        HIPCHECK(hipModuleGetFunction(&r->fn, r->mod, "cep_nfa_jit"));
+      }
       s->qs.push_back(std::move(r));
     }
   });

@@ -65,6 +65,43 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
   const uint64_t tile_hi = tile_lo + kStTile < A.n_events ? tile_lo + kStTile : A.n_events;
   const int64_t rel0 = (int64_t)tile_lo - HV;
 
+  // issue this thread's column loads first: they do not depend on the key boundaries
+  const uint64_t p0 = tile_lo + (uint64_t)tid * kStPer;  // first event of this thread
+  int32_t v[NCOL][kStPer + HV];
+  if (RANGE && p0 < tile_hi) {
+#pragma unroll
+    for (int c = 0; c < NCOL; c++) {
+      const int32_t* col = A.col[c];
+      if (p0 + kStPer <= A.n_events) {
+        const int4* src = reinterpret_cast<const int4*>(col + p0);
+#pragma unroll
+        for (int q = 0; q < kStPer / 4; q++) {
+          const int4 x = src[q];
+          v[c][HV + 4 * q + 0] = x.x;
+          v[c][HV + 4 * q + 1] = x.y;
+          v[c][HV + 4 * q + 2] = x.z;
+          v[c][HV + 4 * q + 3] = x.w;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kStPer; i++) v[c][HV + i] = (p0 + i < A.n_events) ? col[p0 + i] : 0;
+      }
+      if (H > 0) {
+        if (p0 >= (uint64_t)HV) {
+          const int4* src = reinterpret_cast<const int4*>(col + p0 - HV);
+#pragma unroll
+          for (int q = (HV - H) / 4; q < HV / 4; q++) {
+            const int4 x = src[q];
+            v[c][4 * q + 0] = x.x; v[c][4 * q + 1] = x.y; v[c][4 * q + 2] = x.z; v[c][4 * q + 3] = x.w;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < HV; i++) v[c][i] = (p0 + i >= (uint64_t)HV) ? col[p0 + i - HV] : 0;
+        }
+      }
+    }
+  }
+
   // starts of the non-empty keys k0.. that begin before tile_hi (k0 = the key holding
   // tile_lo), compacted into LDS cooperatively: at most kStTile + 1 entries
   const int lane = tid & 63, wv = tid >> 6;
@@ -103,45 +140,12 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
     if (toti < (uint32_t)kStThreads) break;
   }
 
-  const uint64_t p0 = tile_lo + (uint64_t)tid * kStPer;  // first event of this thread
   uint32_t P[M];  // bit b: event p0 - H + b satisfies stage predicate
 #pragma unroll
   for (int s = 0; s < M; s++) P[s] = 0;
   uint32_t valid = 0;
   if (p0 < tile_hi) {
     if (RANGE) {
-      int32_t v[NCOL][kStPer + HV];
-#pragma unroll
-      for (int c = 0; c < NCOL; c++) {
-        const int32_t* col = A.col[c];
-        if (p0 + kStPer <= A.n_events) {
-          const int4* src = reinterpret_cast<const int4*>(col + p0);
-#pragma unroll
-          for (int q = 0; q < kStPer / 4; q++) {
-            const int4 x = src[q];
-            v[c][HV + 4 * q + 0] = x.x;
-            v[c][HV + 4 * q + 1] = x.y;
-            v[c][HV + 4 * q + 2] = x.z;
-            v[c][HV + 4 * q + 3] = x.w;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < kStPer; i++) v[c][HV + i] = (p0 + i < A.n_events) ? col[p0 + i] : 0;
-        }
-        if (H > 0) {
-          if (p0 >= (uint64_t)HV) {
-            const int4* src = reinterpret_cast<const int4*>(col + p0 - HV);
-#pragma unroll
-            for (int q = (HV - H) / 4; q < HV / 4; q++) {
-              const int4 x = src[q];
-              v[c][4 * q + 0] = x.x; v[c][4 * q + 1] = x.y; v[c][4 * q + 2] = x.z; v[c][4 * q + 3] = x.w;
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < HV; i++) v[c][i] = (p0 + i >= (uint64_t)HV) ? col[p0 + i - HV] : 0;
-          }
-        }
-      }
 #pragma unroll
       for (int b = 0; b < kStPer + H; b++) {
         const int i = HV - H + b;
@@ -221,36 +225,50 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
     if (w < wv) woff += s_wsum[w];
     agg += s_wsum[w];
   }
-  // decoupled look-back for the tile's global offset
-  if (tid == 0) {
+  // decoupled look-back for the tile's global offset, one wavefront reading 64 predecessor
+  // status granules per step: it stops at the nearest inclusive prefix and sums the
+  // aggregates in between, spinning only while a nearer predecessor has not published
+  if (wv == 0) {
     unsigned long long excl = 0;
-    if (t == 0) {
-      __hip_atomic_store(&A.status[0], (2ull << 62) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&A.status[t], (1ull << 62) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t pp = (int64_t)t - 1;
+    if (lane == 0)
+      __hip_atomic_store(&A.status[t], ((t == 0 ? 2ull : 1ull) << 62) | agg, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (t > 0) {
+      int64_t base = (int64_t)t - 1;
       uint32_t spins = 0;
-      while (pp >= 0) {
-        const unsigned long long s = __hip_atomic_load(&A.status[pp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long flag = s >> 62;
-        if (flag == 0) {
+      for (;;) {
+        const int64_t idx = base - lane;
+        const unsigned long long s =
+            idx >= 0 ? __hip_atomic_load(&A.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : (2ull << 62);  // before tile 0: inclusive prefix 0
+        const uint32_t flag = (uint32_t)(s >> 62);
+        const uint64_t inc = __ballot(flag == 2), zero = __ballot(flag == 0);
+        const int first = inc ? __builtin_ctzll(inc) : 64;
+        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);  // lanes 0..first
+        if (zero & upto) {
           // predecessors took their tickets earlier, so they are resident and will publish;
           // the bound only turns a bug into a reported error instead of a hang
-          if (++spins > (1u << 24)) {
-            atomicOr(A.overflow, 2u);
+          if (++spins > (1u << 22)) {
+            if (lane == 0) atomicOr(A.overflow, 2u);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        excl += s & ((1ull << 62) - 1);
-        if (flag == 2) break;
-        pp--;
+        unsigned long long v = ((upto >> lane) & 1) ? (s & ((1ull << 62) - 1)) : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        excl += __shfl(v, 0, 64);
+        if (first < 64) break;
+        base -= 64;
       }
-      __hip_atomic_store(&A.status[t], (2ull << 62) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(&A.status[t], (2ull << 62) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_excl = excl;
-    if (t == n_tiles - 1) *A.total = excl + agg;
+    if (lane == 0) {
+      s_excl = excl;
+      if (t == n_tiles - 1) *A.total = excl + agg;
+    }
   }
   __syncthreads();
   uint64_t o = s_excl + woff + (incl - cnt);

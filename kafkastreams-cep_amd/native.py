@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libcep.so")
 
 CEP_MEM_HOST, CEP_MEM_DEVICE = 0, 1
 CEP_KIND_NFA, CEP_KIND_STENCIL = 0, 1
+CEP_TIER_JIT, CEP_TIER_INTERP = 0, 1
 KEY_ERRORS = {0: None, 1: "NullPointerException", 2: "IllegalStateException",
               3: "ArithmeticException", 16: "capacity"}
 
@@ -23,7 +24,7 @@ EXPORTS = [
     "cep_session_create", "cep_session_destroy", "cep_push_batch", "cep_sync", "cep_poll_matches",
     "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
-    "cep_synth_count", "cep_synth_generate",
+    "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
 ]
 
 
@@ -34,7 +35,7 @@ class QueryInfo(C.Structure):
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int), ("force_nfa", C.c_int), ("max_runs", C.c_uint32),
+    _fields_ = [("device", C.c_int), ("force_nfa", C.c_int), ("tier", C.c_int), ("max_runs", C.c_uint32),
                 ("pool_factor", C.c_double)]
 
 
@@ -66,6 +67,8 @@ def lib():
             "cep_query_info_get": ([vp, C.POINTER(QueryInfo)], C.c_int),
             "cep_query_stage_name": ([vp, u32], C.c_char_p),
             "cep_query_destroy": ([vp], None),
+            "cep_query_jit_source": ([vp], C.c_char_p),
+            "cep_jit_precompile": ([vp, C.POINTER(C.c_double)], C.c_int),
             "cep_session_create": ([C.POINTER(vp), C.c_int, C.POINTER(Opts), C.POINTER(vp)], C.c_int),
             "cep_session_destroy": ([vp], None),
             "cep_push_batch": ([vp, C.POINTER(Batch)], C.c_int),
@@ -114,6 +117,16 @@ class Query:
     @property
     def kind(self):
         return self.info.kind
+
+    @property
+    def jit_source(self) -> str:
+        return lib().cep_query_jit_source(self.h).decode()
+
+    def precompile(self) -> float:
+        """Compile the JIT kernel into the code-object cache (no GPU needed); seconds spent."""
+        t = C.c_double()
+        _check(lib().cep_jit_precompile(self.h, C.byref(t)))
+        return t.value
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -193,12 +206,12 @@ class Session:
     """cep_session: per-key NFA state for one or more queries on one GPU."""
 
     def __init__(self, queries, device: int = 0, force_nfa: bool = False, max_runs: int = 0,
-                 pool_factor: float = 0.0):
+                 pool_factor: float = 0.0, tier: int = CEP_TIER_JIT):
         if isinstance(queries, Query):
             queries = [queries]
         self.queries = list(queries)
         arr = (C.c_void_p * len(self.queries))(*[q.h.value for q in self.queries])
-        opts = Opts(device, 1 if force_nfa else 0, max_runs, pool_factor)
+        opts = Opts(device, 1 if force_nfa else 0, tier, max_runs, pool_factor)
         h = C.c_void_p()
         _check(lib().cep_session_create(arr, len(self.queries), C.byref(opts), C.byref(h)))
         self.h = h

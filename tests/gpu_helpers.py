@@ -7,9 +7,9 @@ from kafkastreams_cep_amd import native as N
 from kafkastreams_cep_amd import workloads as W
 
 
-def gpu_run(ir, key_off, cols, force_nfa=False, ts=None, session=None):
+def gpu_run(ir, key_off, cols, force_nfa=False, ts=None, session=None, tier=N.CEP_TIER_JIT):
     q = N.Query(ir)
-    s = session or N.Session(q, force_nfa=force_nfa)
+    s = session or N.Session(q, force_nfa=force_nfa, tier=tier)
     s.push(key_off, cols, ts)
     m = s.matches(0)
     code, seq = s.key_errors(0)

@@ -14,17 +14,19 @@ from kafkastreams_cep_amd import native as N
 from kafkastreams_cep_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
+TIERS = [N.CEP_TIER_JIT, N.CEP_TIER_INTERP]
 
 NFA_CASES = [n for n in kats() if n in STRING_KATS or n in STOCK_KATS]
 
 
+@pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("force_nfa", [False, True])
 @pytest.mark.parametrize("name", NFA_CASES)
-def test_reference_kats_on_gpu(name, force_nfa):
+def test_reference_kats_on_gpu(name, force_nfa, tier):
     case = kats()[name]
     q, off, cols = build_case(name, case)
     ir = q.to_ir()
-    g = gpu_run(ir, off, cols, force_nfa=force_nfa)
+    g = gpu_run(ir, off, cols, force_nfa=force_nfa, tier=tier)
     assert int(g["err_code"][0]) == 0
     if "expected_count" in case:
         assert g["n_matches"] == case["expected_count"]
@@ -41,12 +43,13 @@ def test_strict_kat_uses_stencil():
     assert gpu_run(q.to_ir(), off, cols)["kind"] == N.CEP_KIND_STENCIL
 
 
+@pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("force_nfa", [False, True])
-def test_cfg2_strict_abc_small(force_nfa):
+def test_cfg2_strict_abc_small(force_nfa, tier):
     cfg = W.SynthConfig("t", "abc", 300, 400, 0xCE90000 + 2)
     off, cols = W.generate(cfg)
     ir = W.strict_abc_query().to_ir()
-    assert_parity(gpu_run(ir, off, cols, force_nfa=force_nfa), oracle.run(ir, off, cols, threads=8), off)
+    assert_parity(gpu_run(ir, off, cols, force_nfa=force_nfa, tier=tier), oracle.run(ir, off, cols, threads=8), off)
 
 
 def test_stencil_many_short_keys():
@@ -60,8 +63,9 @@ def test_stencil_many_short_keys():
     assert_parity(gpu_run(ir, off, [v]), oracle.run(ir, off, [v], threads=8), off)
 
 
+@pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("variant", ["readme", "test", "demo"])
-def test_cfg3_stock_small(variant):
+def test_cfg3_stock_small(variant, tier):
     cfg = W.SynthConfig("t", "stock", 1500, 1000, 0xCE90000 + 3)
     off, cols = W.generate(cfg, np.arange(0, 1_000_000, 667)[:1500])
     if variant == "demo":
@@ -69,14 +73,15 @@ def test_cfg3_stock_small(variant):
     ir = W.stock_query(variant).to_ir()
     r = oracle.run(ir, off, cols, threads=8)
     assert r["n_matches"] > 100
-    assert_parity(gpu_run(ir, off, cols), r, off)
+    assert_parity(gpu_run(ir, off, cols, tier=tier), r, off)
 
 
-def test_cfg4_any_kleene_small():
+@pytest.mark.parametrize("tier", TIERS)
+def test_cfg4_any_kleene_small(tier):
     cfg = W.SynthConfig("t", "stock", 400, 300, 0xCE90000 + 4)
     off, cols = W.generate(cfg)
     ir = W.any_kleene_query().to_ir()
-    assert_parity(gpu_run(ir, off, cols), oracle.run(ir, off, cols, threads=8), off)
+    assert_parity(gpu_run(ir, off, cols, tier=tier), oracle.run(ir, off, cols, threads=8), off)
 
 
 def test_cfg5_multi_query_session():
@@ -93,14 +98,19 @@ def test_cfg5_multi_query_session():
         assert s.digest(i)[0] == r["n_matches"]
 
 
-@pytest.mark.parametrize("seed", range(0, 160))
-def test_fuzz_queries_vs_oracle(seed):
+FUZZ_SEEDS = range(0, 160)
+FUZZ_JIT_SEEDS = range(0, 160, 2)  # every JIT query is its own compiled kernel (cached by build())
+
+
+@pytest.mark.parametrize("tier,seed", [(N.CEP_TIER_INTERP, s) for s in FUZZ_SEEDS] +
+                         [(N.CEP_TIER_JIT, s) for s in FUZZ_JIT_SEEDS])
+def test_fuzz_queries_vs_oracle(seed, tier):
     q = random_query(seed)
     ir = q.to_ir()
     if oracle.compile_check(ir):
         pytest.skip("reference compile-time exception")
     off, cols = random_stream(seed, 60, 14)
-    assert_parity(gpu_run(ir, off, cols), oracle.run(ir, off, cols), off)
+    assert_parity(gpu_run(ir, off, cols, tier=tier), oracle.run(ir, off, cols), off)
 
 
 def test_edge_cases_empty_and_single():
