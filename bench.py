@@ -2,7 +2,7 @@
 """bench.py — events/sec of the README stock Kleene+ query on 1/2/4/8 MI355X.
 
 BASELINE.json metric: "events/sec (whole node) + matches/sec, stock Kleene+ query, 1M keys,
-1/2/4/8 GPU".  One step = one pass of the matcher (libcep.so: nfa_kernel + compaction) over
+1/2/4/8 GPU".  One step = one pass of the matcher (libcep.so: cep_nfa_jit + compaction) over
 one batch of 1M keys x ~1000 events per GPU (config 3's shape), inputs already
 resident in HBM, every key starting from the NFA's initial state.  Keys are sharded across
 ranks with no data-path collective (weak scaling: each rank owns its own 1M keys); RCCL only
@@ -12,7 +12,7 @@ all-gathers counts/checksums and reduces the watermark.
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
 Prints ONE JSON line on rank 0 (contract in the task statement; fields documented in
-DESIGN.md §7).  `roofline` prices nfa_kernel at SURVEY §8(d)'s algorithmic bytes (columns read
+DESIGN.md §7).  `roofline` prices cep_nfa_jit at SURVEY §8(d)'s algorithmic bytes (columns read
 once + 4 B per emitted event id + 4 B per match) against 8 TB/s; `cpu_baseline` times the
 oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/64 key
 sample on this host's cores.
@@ -132,7 +132,7 @@ def cpu_baseline(cfg, variant, threads, every):
 
 
 def secondary_strict(device, steps, warmup, dist):
-    """Config 2: strict SEQ(A,B,C), 1e8 events over 1e4 keys, stencil_kernel."""
+    """Config 2: strict SEQ(A,B,C), 1e8 events over 1e4 keys, the three stencil passes."""
     cfg = W.CONFIGS[2]
     stream = N.synth_stream("abc", cfg.seed, cfg.n_keys, cfg.mean_events, 0, device)
     q = N.Query(W.strict_abc_query().to_ir())
@@ -146,7 +146,7 @@ def secondary_strict(device, steps, warmup, dist):
            "ms_per_step": 1e3 * el / steps,
            "roofline": {"bound": "hbm", "achieved": alg / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": load_traffic("stencil_kernel"), "kernel": "stencil_kernel",
+                        "traffic": load_traffic("stencil"), "kernel": "stencil_mask+stencil_scan+stencil_emit",
                         "kernel_ms": kms, "algorithmic_bytes": alg}}
     s.close()
     return res
@@ -211,8 +211,8 @@ def main():
                        "matches_per_gpu_step": int(n_m), "parallelism": f"key-sharded x{dist.world}",
                        "key_errors": int(per[:, 5].sum())},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("nfa_kernel"),
-                         "kernel": "nfa_kernel", "kernel_ms": kms, "compaction_ms": aux_ms,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("cep_nfa_jit"),
+                         "kernel": "cep_nfa_jit", "kernel_ms": kms, "compaction_ms": aux_ms,
                          "algorithmic_bytes": alg},
             "watermark": wm,
         }

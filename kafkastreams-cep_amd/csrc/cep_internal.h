@@ -33,15 +33,17 @@ struct StencilArgs;
 struct KeyState;
 
 hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
-size_t rec_size(int F);
+uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap);  // double-buffered run queues
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
                           const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
-                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals,
-                          unsigned long long* digest, hipStream_t st);
-hipError_t launch_tile_first_key(const uint64_t* key_off, uint64_t n_keys, uint32_t* tile_key, uint64_t n_events,
-                                 hipStream_t st);
+                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals, hipStream_t st);
+hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, const uint32_t* m_key,
+                         const uint32_t* m_emit, const uint64_t* m_off, const uint32_t* p_seq,
+                         const uint16_t* p_stage, unsigned long long* out, hipStream_t st);
+hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* rank,
+                            uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd, uint32_t* tile_rank, hipStream_t st);
 hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
 uint64_t stencil_tiles(uint64_t n_events);
 hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, const uint64_t* key_off,

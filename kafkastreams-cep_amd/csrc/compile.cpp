@@ -506,7 +506,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "  int64_t ts;\n};\n";
   o += "struct Fo {\n  int64_t v[F];\n  uint32_t nm;\n};\n";
   o += "struct Top {\n  uint32_t stage, event, ev_first;\n};\n";
-  o += "struct Out {\n  int produced;\n  Rec<F>* same;\n};\n\n";
+  o += "struct Out {\n  int produced;\n  int same;  // slot of the output record that keeps the run's sequence id\n};\n\n";
   o += "__device__ __forceinline__ void load_ev(Ev& ev, const NfaArgs& A, uint64_t pos) {\n";
   for (uint32_t f = 0; f < d.n_fields; f++)
     if (fields[f])
@@ -551,6 +551,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   const DevStage& bs = d.st[d.begin_stage];
   const bool quiet = bs.n_edges == 1 && bs.e[0].op == OP_BEGIN;
   o += "  static constexpr bool quiet = " + std::string(quiet ? "true" : "false") + ";\n";
+  o += "  static constexpr bool kBeginReg = quiet;\n";
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
   o += "  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {\n    if (sw & kRecEps) return (sw >> 8) & 0xFF;\n    switch (sw & 0xFF) {\n";
@@ -598,8 +599,8 @@ static std::string generate_jit(cep_query* q, Builder& b) {
       const std::string m = "m" + std::to_string(e);
       if (E.op == OP_TAKE) {
         f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        Rec<F>* r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver);\n";
-        f += "        if (!r) return;\n        o.same = r;\n        o.produced++;\n";
+        f += "        const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver);\n";
+        f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n";
         f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      } else {\n";
         f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
         f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2);\n      }\n";
@@ -607,13 +608,13 @@ static std::string generate_jit(cep_query* q, Builder& b) {
       } else if (E.op == OP_BEGIN) {
         const bool fin = d.st[E.target].type == ST_FINAL;
         f += "    if (" + m + ") {\n      L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n";
-        f += "      Rec<F>* r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
+        f += "      const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
              (fin ? " | kRecFinal" : "") + ", L.j, CEP_NONE, ver);\n";
-        f += "      if (!r) return;\n      o.same = r;\n      o.produced++;\n      consumed = true;\n    }\n";
+        f += "      if (r < 0) return;\n      o.same = r;\n      o.produced++;\n      consumed = true;\n    }\n";
       } else if (E.op == OP_IGNORE) {
         f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        Rec<F>* r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver);\n";
-        f += "        if (!r) return;\n        o.same = r;\n        o.produced++;\n      }\n      ignored = true;\n    }\n";
+        f += "        const int r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver);\n";
+        f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n      }\n      ignored = true;\n    }\n";
       } else {  // PROCEED
         const DevStage& T = d.st[E.target];
         const std::string TI = std::to_string(E.target);
@@ -630,14 +631,14 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     }
     f += "    if (br) {\n      if (prev_sk == kNoSk) { L.err = KE_NPE; return; }\n";
     f += "      Dewey v2 = ver;\n      if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
-    f += "      Rec<F>* r = L.push_rec(kRecEps | kRecBranch | (prev_sk << 8) | " + SI +
-         "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2);\n      if (!r) return;\n";
-    f += "      uint32_t nm = (1u << F) - 1;\n";
+    f += "      const int r = L.push_rec(kRecEps | kRecBranch | (prev_sk << 8) | " + SI +
+         "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2);\n      if (r < 0) return;\n";
+    f += "      uint32_t nm = (1u << F) - 1;\n      int64_t fv[F];\n      for (int s = 0; s < F; s++) fv[s] = 0;\n";
     for (int a = 0; a < S.n_aggs; a++) {
       const std::string si = std::to_string(S.agg_state[a]);
-      f += "      if (!((w.nm >> " + si + ") & 1u)) { r->fold[" + si + "] = w.v[" + si + "]; nm &= ~(1u << " + si + "); }\n";
+      f += "      if (!((w.nm >> " + si + ") & 1u)) { fv[" + si + "] = w.v[" + si + "]; nm &= ~(1u << " + si + "); }\n";
     }
-    f += "      r->nullmask = nm;\n      o.produced++;\n";
+    f += "      L.set_folds(r, fv, nm);\n      o.produced++;\n";
     f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
     if (S.n_aggs) {
       f += "    if (consumed) {\n";
@@ -651,7 +652,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "  template <class LT>\n  __device__ __forceinline__ int step(LT& L, const Rec<F>& c) {\n";
   o += "    Ev ev;\n    load_ev(ev, A, L.base + L.j);\n    Fo w;\n";
   o += "    for (int s = 0; s < F; s++) w.v[s] = c.fold[s];\n    w.nm = c.nullmask;\n";
-  o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, nullptr};\n";
+  o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
   o += "    if (c.stage & kRecEps) {\n      const uint32_t esk = (c.stage >> 8) & 0xFF;\n      switch (c.stage & 0xFF) {\n";
   for (uint32_t s = 0; s < d.n_stages; s++) {
@@ -665,11 +666,11 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "        default: L.err = KE_CAPACITY; return -1;\n      }\n    } else {\n";
   o += "      E" + std::to_string(d.begin_stage) + "(L, top, c.ver, brf, kNoSk, ev, w, o);\n    }\n";
   o += "    if (L.err) return -1;\n";
-  o += "    if (o.same) {\n      for (int s = 0; s < F; s++) o.same->fold[s] = w.v[s];\n      o.same->nullmask = w.nm;\n    }\n";
+  o += "    if (o.same >= 0) L.set_folds(o.same, w.v, w.nm);\n";
   o += "    if (!(c.stage & kRecEps)) {  // begin state re-added with a new run (NFA.java:148-157)\n";
   o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = KE_CAPACITY; return -1; }\n";
-  o += "      Rec<F>* r = L.push_rec(c.stage & 0xFF, CEP_NONE, CEP_NONE, v);\n      if (!r) return -1;\n";
-  o += "      r->nullmask = (1u << F) - 1;\n      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
+  o += "      if (!L.readd_begin(c.stage & 0xFF, v)) return -1;\n";
+  o += "      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
   o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256) cep_nfa_jit(NfaArgs A) {\n";
   o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n}  // namespace cep\n";
   return o;

@@ -15,6 +15,38 @@ namespace cep {
 // Dewey held in a local stays in registers instead of scratch.
 constexpr int P = kDeweyPairs;
 
+// Each operation first copies its operands through an empty asm: the unrolled selects then
+// pick between register values.  Selecting between loads instead lets LLVM fold them into
+// one load through a computed address, which pins every Dewey it touches in scratch.
+__device__ __forceinline__ Dewey dw_pin(const Dewey& d) {
+  Dewey x;
+  uint32_t n = d.n, len = d.len;
+  asm("" : "+v"(n), "+v"(len));
+  x.n = n;
+  x.len = len;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    int32_t a = d.v[k];
+    uint32_t b = d.c[k];
+    asm("" : "+v"(a), "+v"(b));
+    x.v[k] = a;
+    x.c[k] = b;
+  }
+  return x;
+}
+
+// field-wise store (a struct copy from a local would be lowered through scratch)
+__device__ __forceinline__ void dw_store(Dewey& dst, const Dewey& v) {
+  const Dewey x = dw_pin(v);
+  dst.n = x.n;
+  dst.len = x.len;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    dst.v[k] = x.v[k];
+    dst.c[k] = x.c[k];
+  }
+}
+
 __device__ __forceinline__ void dw_init(Dewey& d, int32_t v) {
   d.n = 1;
   d.len = 1;
@@ -27,7 +59,8 @@ __device__ __forceinline__ void dw_init(Dewey& d, int32_t v) {
   }
 }
 
-__device__ __forceinline__ int32_t dw_last(const Dewey& d) {
+__device__ __forceinline__ int32_t dw_last(const Dewey& d0) {
+  const Dewey d = dw_pin(d0);
   int32_t r = d.v[0];
 #pragma unroll
   for (int k = 1; k < P; k++)
@@ -36,7 +69,8 @@ __device__ __forceinline__ int32_t dw_last(const Dewey& d) {
 }
 
 // last digit + 1; false when the RLE would need more than kDeweyPairs pairs
-__device__ __forceinline__ bool dw_add_run(Dewey& d) {
+__device__ __forceinline__ bool dw_add_run(Dewey& d0) {
+  Dewey d = dw_pin(d0);
   const uint32_t i = d.n - 1;
   uint32_t ci = 0;
   int32_t vi = 0, vprev = 0;
@@ -57,6 +91,7 @@ __device__ __forceinline__ bool dw_add_run(Dewey& d) {
       if (merge && (uint32_t)k + 1 == i) d.c[k] += 1;
     }
     if (merge) d.n--;
+    d0 = d;
     return true;
   }
   if (d.n >= (uint32_t)P) return false;
@@ -69,11 +104,13 @@ __device__ __forceinline__ bool dw_add_run(Dewey& d) {
     }
   }
   d.n++;
+  d0 = d;
   return true;
 }
 
 // append digit 0
-__device__ __forceinline__ bool dw_add_stage(Dewey& d) {
+__device__ __forceinline__ bool dw_add_stage(Dewey& d0) {
+  Dewey d = dw_pin(d0);
   const uint32_t i = d.n - 1;
   const int32_t vi = dw_last(d);
   if (vi == 0) {
@@ -81,6 +118,7 @@ __device__ __forceinline__ bool dw_add_stage(Dewey& d) {
     for (int k = 0; k < P; k++)
       if ((uint32_t)k == i) d.c[k] += 1;
     d.len++;
+    d0 = d;
     return true;
   }
   if (d.n >= (uint32_t)P) return false;
@@ -92,11 +130,13 @@ __device__ __forceinline__ bool dw_add_stage(Dewey& d) {
     }
   d.n++;
   d.len++;
+  d0 = d;
   return true;
 }
 
 // this.isCompatible(that)  (a = this, b = that)
-__device__ __forceinline__ bool dw_compatible(const Dewey& a, const Dewey& b) {
+__device__ __forceinline__ bool dw_compatible(const Dewey& a0, const Dewey& b0) {
+  const Dewey a = dw_pin(a0), b = dw_pin(b0);
   if (a.len > b.len) {
     // b is a prefix of a: b's pairs but the last equal a's, b's last run is a prefix of a's run
     if (b.n > a.n) return false;

@@ -37,6 +37,7 @@ struct InterpQ {
   const NfaArgs& A;
   bool quiet;
   uint32_t begin_stage;
+  static constexpr bool kBeginReg = false;  // quiet is only known at run time here
 
   __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {
     begin_stage = q.begin_stage;
@@ -73,7 +74,7 @@ struct InterpQ {
     const uint32_t top_sk = stage_sk(top);
     const uint32_t j = lane.j;
     int produced = 0;
-    Rec<F>* same_seq = nullptr;  // the (single) output record that keeps this run's sequence id
+    int same_seq = -1;  // slot of the (single) output record that keeps this run's sequence id
 
     uint8_t lv_cur[kMaxStages + 1];
     uint8_t lv_prev[kMaxStages + 1];
@@ -125,8 +126,8 @@ struct InterpQ {
             proceed_target = E.target;
           } else if (E.op == OP_TAKE) {
             if (!br) {  // newEpsilonState(current, current), same run
-              Rec<F>* r = lane.push_rec(kRecEps | (cur_sk << 8) | cur, j, CEP_NONE, ver);
-              if (!r) return -1;
+              const int r = lane.push_rec(kRecEps | (cur_sk << 8) | cur, j, CEP_NONE, ver);
+              if (r < 0) return -1;
               same_seq = r;
               produced++;
               lane.put_link(cur_sk, lv_prev[L], c.event, c.ev_first, ver);
@@ -142,16 +143,16 @@ struct InterpQ {
             if (lane.err) return -1;
             uint32_t sw = kRecEps | (cur_sk << 8) | E.target;
             if (q.st[E.target].type == ST_FINAL) sw |= kRecFinal;
-            Rec<F>* r = lane.push_rec(sw, j, CEP_NONE, ver);
-            if (!r) return -1;
+            const int r = lane.push_rec(sw, j, CEP_NONE, ver);
+            if (r < 0) return -1;
             same_seq = r;
             produced++;
             lv_flags[L] |= 4;
           } else {  // IGNORE: re-add the context record (top stage/event, this level's version)
             if (!br) {
-              Rec<F>* r = lane.push_rec((top & ~(kRecBranch | kRecFinal)) | ((lv_flags[L] & 1) ? kRecBranch : 0),
-                                        c.event, c.ev_first, ver);
-              if (!r) return -1;
+              const int r = lane.push_rec((top & ~(kRecBranch | kRecFinal)) | ((lv_flags[L] & 1) ? kRecBranch : 0),
+                                          c.event, c.ev_first, ver);
+              if (r < 0) return -1;
               same_seq = r;
               produced++;
             }
@@ -184,20 +185,25 @@ struct InterpQ {
         if (lv_prev[l] == kNoSk) { lane.err = KE_NPE; return -1; }  // newEpsilonState(null, ...)
         Dewey v2 = ver;
         if (!dw_add_run(v2)) { lane.err = KE_CAPACITY; return -1; }
-        Rec<F>* r = (fl & 8) ? lane.push_rec(kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur, c.event,
+        const int r = (fl & 8) ? lane.push_rec(kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur, c.event,
                                              c.ev_first, v2)
                              : lane.push_rec(kRecEps | kRecBranch | ((uint32_t)lv_prev[l] << 8) | cur, j,
                                              CEP_NONE, v2);
-        if (!r) return -1;
+        if (r < 0) return -1;
         uint32_t nm = (1u << F) - 1;  // fresh sequence: only this stage's aggregates are copied
+        int64_t fv[F];
+#pragma unroll
+        for (int s = 0; s < F; s++) fv[s] = 0;
         for (int a = 0; a < S.n_aggs; a++) {
           const uint32_t s = S.agg_state[a];
           if (!((wnull >> s) & 1u)) {
-            r->fold[s] = W[s];
+#pragma unroll
+            for (int t = 0; t < F; t++)
+              if ((uint32_t)t == s) fv[t] = W[t];
             nm &= ~(1u << s);
           }
         }
-        r->nullmask = nm;
+        lane.set_folds(r, fv, nm);
         produced++;
         lane.walk_branch(lv_prev[l], c.event, c.ev_first, ver);
         if (lane.err) return -1;
@@ -216,17 +222,12 @@ struct InterpQ {
         }
       }
     }
-    if (same_seq) {
-      for (int s = 0; s < F; s++) same_seq->fold[s] = W[s];
-      same_seq->nullmask = wnull;
-    }
+    if (same_seq >= 0) lane.set_folds(same_seq, W, wnull);
     // begin state re-added with a new run (:148-157)
     if (!top_eps && q.st[top & 0xFF].type == ST_BEGIN) {
       Dewey v = c.ver;
       if (produced > 0 && !dw_add_run(v)) { lane.err = KE_CAPACITY; return -1; }
-      Rec<F>* r = lane.push_rec(top & 0xFF, CEP_NONE, CEP_NONE, v);
-      if (!r) return -1;
-      r->nullmask = (1u << F) - 1;
+      if (!lane.readd_begin(top & 0xFF, v)) return -1;
       produced++;
     }
     return produced;
@@ -316,7 +317,7 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
                                                        const uint64_t* bsum_p, const uint32_t* out,
                                                        uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
                                                        uint32_t* p_seq, uint16_t* p_stage,
-                                                       const uint64_t* totals, unsigned long long* digest) {
+                                                       const uint64_t* totals) {
   __shared__ uint64_t sm[256], sp[256];
   const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t nm = k < n ? ks[k].n_matches : 0, npairs = k < n ? ks[k].n_pairs : 0;
@@ -337,7 +338,6 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
   if (k == 0) m_off[totals[0]] = totals[1];
   if (nm == 0) return;
   uint32_t chunk = ks[k].out_first, pos = 0;
-  uint64_t dsum = 0;
   auto next = [&]() -> uint32_t {
     if (pos == kOutChunkWords - 1) {
       chunk = out[(uint64_t)chunk * kOutChunkWords + kOutChunkWords - 1];
@@ -351,19 +351,50 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
     m_key[mo] = (uint32_t)k;
     m_emit[mo] = emit;
     m_off[mo] = po;
-    uint64_t h = mix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)k << 32) ^ emit);
     for (uint32_t i = 0; i < np; i++) {
       const uint32_t s = next();
       const uint32_t st = next();
       p_seq[po] = s;
       p_stage[po] = (uint16_t)st;
-      h = mix64(h ^ (((uint64_t)st << 32) | s));
       po++;
     }
-    dsum += h;
     mo++;
   }
-  atomicAdd(digest, (unsigned long long)dsum);
+}
+
+// order-independent checksum of the flat match arrays (tests/gpu_helpers.py, bench.py and
+// multi-GPU all-gather): Σ_match mix(mix(C ^ key << 32 ^ emit) ^ (stage << 32 | seq) ...),
+// the same function as workloads.match_digest.  Fixed arity (m_emit == nullptr): match i's
+// pairs are p_seq[i m .. i m + m) with stage names `names`, emit = its first pair.
+struct DigestNames {
+  uint16_t v[8];
+};
+
+__global__ void __launch_bounds__(256) digest_matches(uint64_t n, uint32_t arity, DigestNames names,
+                                                      const uint32_t* m_key, const uint32_t* m_emit,
+                                                      const uint64_t* m_off, const uint32_t* p_seq,
+                                                      const uint16_t* p_stage, unsigned long long* out) {
+  __shared__ unsigned long long sd[4];
+  unsigned long long dsum = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    uint64_t h;
+    if (arity) {
+      const uint32_t* ps = p_seq + i * arity;
+      h = mix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)m_key[i] << 32) ^ ps[0]);
+      for (uint32_t x = 0; x < arity && x < 8; x++) h = mix64(h ^ (((uint64_t)names.v[x] << 32) | ps[x]));
+    } else {
+      h = mix64(0x9E3779B97F4A7C15ull ^ ((uint64_t)m_key[i] << 32) ^ m_emit[i]);
+      for (uint64_t p = m_off[i]; p < m_off[i + 1]; p++) h = mix64(h ^ (((uint64_t)p_stage[p] << 32) | p_seq[p]));
+    }
+    dsum += h;
+  }
+  for (int off = 32; off > 0; off >>= 1) dsum += __shfl_down(dsum, off, 64);
+  if ((threadIdx.x & 63) == 0) sd[threadIdx.x >> 6] = dsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long d = sd[0] + sd[1] + sd[2] + sd[3];
+    if (d) atomicAdd(out, d);
+  }
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -384,12 +415,8 @@ hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_le
   }
 }
 
-size_t rec_size(int F) {
-  switch (F) {
-    case 0: case 1: case 2: return sizeof(Rec<2>);
-    case 3: case 4: return sizeof(Rec<4>);
-    default: return sizeof(Rec<8>);
-  }
+uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap) {
+  return ring_bytes(F <= 2 ? 2 : (F <= 4 ? 4 : 8), n_slots, rcap);
 }
 
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
@@ -404,11 +431,24 @@ hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m,
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
                           const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
                           uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals,
-                          unsigned long long* digest, hipStream_t st) {
+                          hipStream_t st) {
   const uint64_t nb = (n_keys + 255) / 256;
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_matches, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p, out,
-                     m_key, m_emit, m_off, p_seq, p_stage, totals, digest);
+                     m_key, m_emit, m_off, p_seq, p_stage, totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, const uint32_t* m_key,
+                         const uint32_t* m_emit, const uint64_t* m_off, const uint32_t* p_seq,
+                         const uint16_t* p_stage, unsigned long long* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  DigestNames nm{};
+  for (uint32_t x = 0; x < arity && x < 8; x++) nm.v[x] = names[x];
+  const uint64_t want = (n + 255) / 256;
+  const uint32_t blocks = (uint32_t)(want < 1024 ? want : 1024);
+  hipLaunchKernelGGL(digest_matches, dim3(blocks), dim3(256), 0, st, n, arity, nm, m_key, m_emit, m_off, p_seq,
+                     p_stage, out);
   return hipGetLastError();
 }
 

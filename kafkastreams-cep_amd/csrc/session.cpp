@@ -14,6 +14,7 @@
 
 #include "cep_internal.h"
 #include "kernel_args.h"
+#include "stencil_args.h"
 
 using namespace cep;
 
@@ -89,6 +90,7 @@ struct QueryRt {
   DBuf ks;
   uint64_t n_matches = 0, n_pairs = 0;
   unsigned long long digest = 0;
+  bool digest_valid = false;  // computed on demand (cep_match_digest)
   uint32_t arity = 0;
   bool have = false;
   // host copies
@@ -118,7 +120,7 @@ struct cep_session {
   Cols cols{};
   int64_t watermark = INT64_MIN;
   // scratch
-  DBuf rings, nodes, preds, out, scratch, tile_key, status, keylist;
+  DBuf rings, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask;
 };
 
 namespace {
@@ -144,28 +146,38 @@ struct Scratch {  // small counters, one allocation
 void run_stencil(cep_session* s, QueryRt& r) {
   const cep_query* q = r.q;
   const uint32_t m = q->info.arity;
+  const uint64_t nk = s->n_keys;
   const uint64_t n_tiles = stencil_tiles(s->n_events);
-  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));
-  s->status.ensure(sizeof(unsigned long long) * (n_tiles + 1));
+  const uint64_t nb = (nk + 1023) / 1024;
+  s->tile_key.ensure(sizeof(uint32_t) * 2 * (n_tiles + 1));                    // tile rank + count
+  s->status.ensure(sizeof(uint64_t) * (n_tiles + 1));                           // tile offsets
+  s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));
+  s->keylist.ensure(sizeof(uint32_t) * (2 * nk + nb + 2));                       // rank, nz_key, bsum
+  s->bnd.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));
   s->scratch.ensure(sizeof(Scratch));
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
   r.m_key.ensure(sizeof(uint32_t) * cap);
   r.p_seq.ensure(sizeof(uint32_t) * cap * m);
   Scratch* sc = s->scratch.as<Scratch>();
+  uint32_t* rank = s->keylist.as<uint32_t>();
+  uint32_t* nz_key = rank + nk;
+  uint32_t* bsum = nz_key + nk;
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
-  HIPCHECK(hipMemsetAsync(s->status.p, 0, sizeof(unsigned long long) * (n_tiles + 1), s->stream));
   StencilArgs a{};
-  a.n_keys = s->n_keys;
+  a.n_keys = nk;
   a.n_events = s->n_events;
   a.key_off = s->key_off;
-  a.tile_key = s->tile_key.as<uint32_t>();
+  a.bnd = s->bnd.as<uint64_t>();
+  a.tile_rank = s->tile_key.as<uint32_t>();
+  a.nz_key = nz_key;
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.cols = s->cols;
   a.ts = s->ts;
   const bool range = q->stencilRange;
   for (int c = 0; c < 2; c++) a.col[c] = (const int32_t*)s->cols.p[q->rangeCols[c]];
+  a.aligned = ((uintptr_t)a.col[0] % 16 == 0) && ((uintptr_t)a.col[1] % 16 == 0);
   for (uint32_t i = 0; i < m && i < 8; i++) {
     a.prog[i] = q->stencilProg[i];
     for (int c = 0; c < 2; c++) {
@@ -174,16 +186,18 @@ void run_stencil(cep_session* s, QueryRt& r) {
     }
   }
   for (uint32_t x = 0; x < m && x < 8; x++) a.stage_name[x] = q->arityStage[x];
-  a.tile_counter = &sc->tile_counter;
-  a.status = s->status.as<unsigned long long>();
+  a.mask = s->mask.as<uint64_t>();
+  a.tile_cnt = s->tile_key.as<uint32_t>() + (n_tiles + 1);
+  a.tile_off = s->status.as<uint64_t>();
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
   a.total = &sc->total;
-  a.digest = &sc->digest;
   a.out_cap = cap;
   a.overflow = &sc->overflow;
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
-  HIPCHECK(launch_tile_first_key(s->key_off, s->n_keys, s->tile_key.as<uint32_t>(), s->n_events, s->stream));
+  HIPCHECK(hipMemsetAsync(s->bnd.p, 0, sizeof(uint64_t) * (s->n_events / 64 + 2), s->stream));
+  HIPCHECK(launch_key_index(s->key_off, nk, s->n_events, rank, bsum, nz_key, s->bnd.as<uint64_t>(),
+                            s->tile_key.as<uint32_t>(), s->stream));
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
   HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
@@ -192,15 +206,15 @@ void run_stencil(cep_session* s, QueryRt& r) {
   HIPCHECK(hipStreamSynchronize(s->stream));
   HIPCHECK(hipEventElapsedTime(&r.kernel_ms, s->ev0, s->ev1));
   HIPCHECK(hipEventElapsedTime(&r.aux_ms, s->ev2, s->ev0));
-  r.launches = 1;
-  if (h.overflow) throw std::runtime_error(h.overflow & 2 ? "stencil look-back did not complete" : "stencil output overflow");
+  r.launches = 3;  // stencil_mask + stencil_scan + stencil_emit
+  if (h.overflow) throw std::runtime_error("stencil output overflow");
   r.n_matches = h.total;
   r.n_pairs = h.total * m;
-  r.digest = h.digest;
+  r.digest_valid = false;
   r.arity = m;
-  // no per-key errors on this path: the predicates are total
-  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(s->n_keys, 1));
-  HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * s->n_keys, s->stream));
+  // no per-key errors on this path: the predicates and folds are total
+  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
+  HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * nk, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
 }
 
@@ -213,11 +227,9 @@ hipError_t launch_nfa_tier(QueryRt& r, NfaArgs& a, uint64_t nslots, hipStream_t 
 }
 
 void run_nfa(cep_session* s, QueryRt& r) {
-  const cep_query* q = r.q;
   const uint64_t nk = s->n_keys;
   uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
   const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.25;
-  const size_t recsz = rec_size(r.F);
   r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
@@ -233,7 +245,7 @@ void run_nfa(cep_session* s, QueryRt& r) {
   s->nodes.ensure(sizeof(Node) * node_cap);
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
-  s->rings.ensure(recsz * rcap * std::max<uint64_t>(nk, 1));
+  s->rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
@@ -301,7 +313,7 @@ void run_nfa(cep_session* s, QueryRt& r) {
     pred_cap = pn;
     out_cap = on;
     DBuf retry_rings;
-    retry_rings.ensure(recsz * rcap * list.size());
+    retry_rings.ensure(ring_size(r.F, list.size(), rcap));
     HIPCHECK(hipMemcpyAsync(sc, &fix, sizeof fix, hipMemcpyHostToDevice, s->stream));
     a.nodes = s->nodes.as<Node>();
     a.preds = s->preds.as<Pred>();
@@ -343,14 +355,14 @@ void run_nfa(cep_session* s, QueryRt& r) {
   r.p_stage.ensure(sizeof(uint16_t) * (tot[1] + 1));
   HIPCHECK(launch_scatter(r.ks.as<KeyState>(), nk, bm, bp, s->out.as<uint32_t>(), r.m_key.as<uint32_t>(),
                           r.m_emit.as<uint32_t>(), r.m_off.as<uint64_t>(), r.p_seq.as<uint32_t>(),
-                          r.p_stage.as<uint16_t>(), sc->totals, &sc->digest, s->stream));
+                          r.p_stage.as<uint16_t>(), sc->totals, s->stream));
   if (nk == 0) HIPCHECK(hipMemsetAsync(r.m_off.p, 0, sizeof(uint64_t), s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
   HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   r.aux_ms = ms;  // compaction (count/scan/scatter)
-  r.digest = h.digest;
+  r.digest_valid = false;
   r.arity = 0;
   r.kernel_ms = total_ms;  // matching kernel launches only
 }
@@ -606,9 +618,22 @@ int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* c
   if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
   QueryRt& r = *s->qs[query];
   if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
-  if (n_matches) *n_matches = r.n_matches;
-  if (checksum) *checksum = r.digest;
-  return CEP_OK;
+  return guarded([&] {
+    if (checksum && !r.digest_valid) {
+      DeviceGuard g(s->device);
+      s->scratch.ensure(sizeof(Scratch));
+      Scratch* sc = s->scratch.as<Scratch>();
+      HIPCHECK(hipMemsetAsync(&sc->digest, 0, sizeof sc->digest, s->stream));
+      HIPCHECK(launch_digest(r.n_matches, r.arity, r.arity ? r.q->arityStage.data() : nullptr,
+                             r.m_key.as<uint32_t>(), r.m_emit.as<uint32_t>(), r.m_off.as<uint64_t>(),
+                             r.p_seq.as<uint32_t>(), r.p_stage.as<uint16_t>(), &sc->digest, s->stream));
+      HIPCHECK(hipMemcpyAsync(&r.digest, &sc->digest, sizeof r.digest, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipStreamSynchronize(s->stream));
+      r.digest_valid = true;
+    }
+    if (n_matches) *n_matches = r.n_matches;
+    if (checksum) *checksum = r.digest;
+  });
 }
 
 int cep_watermark(cep_session* s, int64_t* out) {

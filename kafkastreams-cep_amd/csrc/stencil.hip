@@ -1,5 +1,5 @@
 // stencil.hip — CEP_KIND_STENCIL: SEQ(p_0, ..., p_{m-1}) with every stage ONE + strict
-// contiguity and total, state-free predicates.
+// contiguity and total, state-free predicates and folds.
 //
 // For such queries the reference NFA (nfa/NFA.java) never branches, each run lives at most
 // m events, and every run's buffer nodes are private; so the matches of a key's stream
@@ -8,33 +8,92 @@
 // (proof: SURVEY Appendix A.5).  That is a 1-D stencil over the column:
 // HBM-bound, one pass.
 //
-// Layout: tile = 256 threads x 16 consecutive events.  A thread reads its 16 int32 values
-// with four 16-B loads (plus the previous vector for the m-1 halo), evaluates the m stage
-// predicates as bit vectors, and ANDs them shifted (match bit i = Π_t P_{m-1-t}(i-t)).
-// Key boundaries come from the CSR offsets (first key of each tile precomputed).  Output
-// order is deterministic: a per-tile decoupled look-back (8-B status granules, agent scope)
-// gives each tile its global output offset in a single pass.
+// Layout.  A tile is 256 threads x 64 consecutive events; a thread reads its 64 int32 values
+// with sixteen 16-B loads (plus the m-1 halo events), evaluates the m stage predicates into
+// 64-bit masks and ANDs them shifted (match bit i = Π_x P_{m-1-x}(i-x)).  Key starts come
+// from a bitmap built once per batch, so a window crossing a key start is masked with
+// shifts, and a match's key is the tile's first key advanced by the key starts before it.
+//
+// Passes.  (1) stencil_mask streams the column once and writes one 64-bit match mask per 64
+// events (1 bit/event) and a count per tile; (2) a single-block scan turns tile counts into
+// output offsets; (3) stencil_emit reads the masks back (1/32 of the column's bytes) and
+// writes the matches in order.  Nothing waits on another workgroup, so the streaming pass
+// runs at HBM rate (a single-pass decoupled look-back was measured latency-bound here:
+// rounds of co-resident tiles look back through each other, profiles/README.md).
 #include <hip/hip_runtime.h>
 
 #include "cep_layout.h"
 #include "nfa_device.h"
+#include "stencil_args.h"
 
 namespace cep {
 
-constexpr int kStTile = 4096;  // events per tile
-constexpr int kStThreads = 256;
-constexpr int kStPer = 16;     // events per thread
+typedef int v4i __attribute__((ext_vector_type(4)));
 
-// tile -> first key: key k writes every tile whose first event lies inside it
-__global__ void __launch_bounds__(256) tile_first_key(const uint64_t* key_off, uint64_t n_keys, uint32_t* tile_key,
-                                                      uint64_t n_tiles) {
+constexpr int kStThreads = 256;
+constexpr int kStPer = 64;  // events per thread (one 64-bit mask)
+constexpr uint64_t kStTile = (uint64_t)kStThreads * kStPer;
+
+// ---------------------------------------------------------------- per-batch key index
+// rank[k] = number of non-empty keys before k (two-level exclusive scan)
+__global__ void __launch_bounds__(1024) nz_rank_blocks(const uint64_t* key_off, uint64_t n_keys, uint32_t* rank,
+                                                       uint32_t* bsum) {
+  __shared__ uint32_t s[1024];
+  const uint64_t k = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t f = (k < n_keys && key_off[k + 1] > key_off[k]) ? 1u : 0u;
+  s[threadIdx.x] = f;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t y = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  if (k < n_keys) rank[k] = s[threadIdx.x] - f;
+  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+
+__global__ void __launch_bounds__(1024) nz_rank_top(uint32_t* bsum, uint64_t nb) {
+  __shared__ uint32_t t[1024];
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t a = threadIdx.x * per, b = (a + per < nb) ? a + per : nb;
+  uint32_t sum = 0;
+  for (uint64_t i = a; i < b; i++) sum += bsum[i];
+  t[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < 1024; i++) {
+      const uint32_t x = t[i];
+      t[i] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+  uint32_t o = t[threadIdx.x];
+  for (uint64_t i = a; i < b; i++) {
+    const uint32_t x = bsum[i];
+    bsum[i] = o;
+    o += x;
+  }
+}
+
+// non-empty key k: nz_key[rank] = k, its start bit, and the rank of every tile whose first
+// event lies inside it
+__global__ void __launch_bounds__(256) key_index(const uint64_t* key_off, uint64_t n_keys, const uint32_t* rank,
+                                                 const uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd,
+                                                 uint32_t* tile_rank, uint64_t n_tiles) {
   const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= n_keys) return;
   const uint64_t s = key_off[k], e = key_off[k + 1];
   if (s == e) return;
-  for (uint64_t t = (s + kStTile - 1) / kStTile; t * kStTile < e && t < n_tiles; t++) tile_key[t] = (uint32_t)k;
+  const uint32_t r = rank[k] + bsum[k / 1024];
+  nz_key[r] = (uint32_t)k;
+  atomicOr((unsigned long long*)&bnd[s / 64], 1ull << (s % 64));
+  for (uint64_t t = (s + kStTile - 1) / kStTile; t * kStTile < e && t < n_tiles; t++) tile_rank[t] = r;
 }
 
+// ---------------------------------------------------------------- the stencil
 __device__ __forceinline__ uint64_t mix64s(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -43,176 +102,191 @@ __device__ __forceinline__ uint64_t mix64s(uint64_t z) {
 
 __device__ __forceinline__ bool in_range(int64_t v, int64_t lo, int64_t hi) { return v >= lo && v <= hi; }
 
+// Pass 1 layout.  A wave owns kStWave consecutive events and reads them with 16-B loads in
+// which lane l holds events 4l..4l+3 of a 256-event step: every load instruction covers
+// 1 KiB contiguous (fully coalesced).  Per step a lane evaluates the M stage predicates
+// into 4-bit nibbles; the window needs the M-1 <= 7 events before the nibble, i.e. the
+// nibbles of lanes l-1 and l-2 (cross-lane shuffles) or, for lanes 0-1, of lanes 62-63 of
+// the previous step (wave-uniform carries).  Key starts come the same way from the bitmap.
+constexpr int kStWave = kStTile / (kStThreads / 64);  // 4096 events per wave
+constexpr int kStSteps = kStWave / 256;               // 16 load steps per wave
+
 template <int M, bool RANGE, int NCOL>
-__global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
-  constexpr int HV = 8;        // halo values loaded before p0 (two 16-B vectors)
-  constexpr int H = M - 1;     // halo events a window needs
-  constexpr int kBnd = kStTile + HV + 1;
-  __shared__ uint32_t s_tile;
-  __shared__ unsigned long long s_excl;
-  __shared__ uint32_t s_bnd[kBnd];   // key starts, relative to tile_lo - HV (sorted)
-  __shared__ uint32_t s_bkey[kBnd];
-  __shared__ uint32_t s_wk[kStThreads / 64], s_wi[kStThreads / 64];
-  __shared__ uint32_t s_wsum[kStThreads / 64];
-  __shared__ unsigned long long s_dig[kStThreads / 64];
-
-  const int tid = threadIdx.x;
-  if (tid == 0) s_tile = atomicAdd(A.tile_counter, 1u);
-  __syncthreads();
-  const uint64_t t = s_tile;
-  const uint64_t n_tiles = (A.n_events + kStTile - 1) / kStTile;
-  const uint64_t tile_lo = t * kStTile;
-  const uint64_t tile_hi = tile_lo + kStTile < A.n_events ? tile_lo + kStTile : A.n_events;
-  const int64_t rel0 = (int64_t)tile_lo - HV;
-
-  // issue this thread's column loads first: they do not depend on the key boundaries
-  const uint64_t p0 = tile_lo + (uint64_t)tid * kStPer;  // first event of this thread
-  int32_t v[NCOL][kStPer + HV];
-  if (RANGE && p0 < tile_hi) {
-#pragma unroll
-    for (int c = 0; c < NCOL; c++) {
-      const int32_t* col = A.col[c];
-      if (p0 + kStPer <= A.n_events) {
-        const int4* src = reinterpret_cast<const int4*>(col + p0);
-#pragma unroll
-        for (int q = 0; q < kStPer / 4; q++) {
-          const int4 x = src[q];
-          v[c][HV + 4 * q + 0] = x.x;
-          v[c][HV + 4 * q + 1] = x.y;
-          v[c][HV + 4 * q + 2] = x.z;
-          v[c][HV + 4 * q + 3] = x.w;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < kStPer; i++) v[c][HV + i] = (p0 + i < A.n_events) ? col[p0 + i] : 0;
-      }
-      if (H > 0) {
-        if (p0 >= (uint64_t)HV) {
-          const int4* src = reinterpret_cast<const int4*>(col + p0 - HV);
-#pragma unroll
-          for (int q = (HV - H) / 4; q < HV / 4; q++) {
-            const int4 x = src[q];
-            v[c][4 * q + 0] = x.x; v[c][4 * q + 1] = x.y; v[c][4 * q + 2] = x.z; v[c][4 * q + 3] = x.w;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < HV; i++) v[c][i] = (p0 + i >= (uint64_t)HV) ? col[p0 + i - HV] : 0;
-        }
-      }
-    }
-  }
-
-  // starts of the non-empty keys k0.. that begin before tile_hi (k0 = the key holding
-  // tile_lo), compacted into LDS cooperatively: at most kStTile + 1 entries
-  const int lane = tid & 63, wv = tid >> 6;
-  const uint32_t k0 = A.tile_key[t];
-  uint32_t nb = 0;
-  for (uint64_t kb = k0;; kb += kStThreads) {
-    const uint64_t k = kb + tid;
-    const bool have = k < A.n_keys;
-    uint64_t s = 0, e = 0;
-    if (have) {
-      s = A.key_off[k];
-      e = A.key_off[k + 1];
-    }
-    const bool inr = have && s < tile_hi;
-    const bool keep = inr && (e > s || k == k0);
-    const uint64_t bk = __ballot(keep), bi = __ballot(inr);
-    if (lane == 0) {
-      s_wk[wv] = (uint32_t)__popcll(bk);
-      s_wi[wv] = (uint32_t)__popcll(bi);
-    }
-    __syncthreads();
-    uint32_t off = nb, tot = 0, toti = 0;
-    for (int w = 0; w < kStThreads / 64; w++) {
-      if (w < wv) off += s_wk[w];
-      tot += s_wk[w];
-      toti += s_wi[w];
-    }
-    if (keep) {
-      const uint32_t idx = off + (uint32_t)__popcll(bk & ((1ull << lane) - 1));
-      const int64_t r = (int64_t)s - rel0;
-      s_bnd[idx] = r < 0 ? 0u : (uint32_t)r;
-      s_bkey[idx] = (uint32_t)k;
-    }
-    nb += tot;
-    __syncthreads();
-    if (toti < (uint32_t)kStThreads) break;
-  }
-
-  uint32_t P[M];  // bit b: event p0 - H + b satisfies stage predicate
-#pragma unroll
-  for (int s = 0; s < M; s++) P[s] = 0;
-  uint32_t valid = 0;
-  if (p0 < tile_hi) {
+struct StEval {
+  int32_t lo[M][2], hi[M][2];
+  __device__ __forceinline__ explicit StEval(const StencilArgs& A) {
     if (RANGE) {
+      // int32 bounds (a range outside int32 is clamped: empty stays empty)
 #pragma unroll
-      for (int b = 0; b < kStPer + H; b++) {
-        const int i = HV - H + b;
-        const int64_t p = (int64_t)p0 - H + b;
-        if (p < 0 || (uint64_t)p >= A.n_events) continue;
-        valid |= 1u << b;
+      for (int s = 0; s < M; s++)
 #pragma unroll
-        for (int s = 0; s < M; s++) {
-          bool ok = in_range(v[0][i], A.rs[s].lo[0], A.rs[s].hi[0]);
-          if (NCOL > 1) ok = ok && in_range(v[NCOL - 1][i], A.rs[s].lo[1], A.rs[s].hi[1]);
-          P[s] |= (ok ? 1u : 0u) << b;
+        for (int c = 0; c < 2; c++) {
+          const int64_t l = A.rs[s].lo[c], h = A.rs[s].hi[c];
+          lo[s][c] = l < INT32_MIN ? INT32_MIN : (l > INT32_MAX ? INT32_MAX : (int32_t)l);
+          hi[s][c] = h > INT32_MAX ? INT32_MAX : (h < INT32_MIN ? INT32_MIN : (int32_t)h);
+          if (l > INT32_MAX || h < INT32_MIN || l > h) {
+            lo[s][c] = 1;
+            hi[s][c] = 0;
+          }
         }
-      }
+    }
+  }
+  // stage bits of one event into bit `bit` of P[s]
+  __device__ __forceinline__ void range(int32_t x0, int32_t x1, uint32_t* P, int bit) const {
+#pragma unroll
+    for (int s = 0; s < M; s++) {
+      bool ok = x0 >= lo[s][0] && x0 <= hi[s][0];
+      if (NCOL > 1) ok = ok && x1 >= lo[s][1] && x1 <= hi[s][1];
+      P[s] |= (ok ? 1u : 0u) << bit;
+    }
+  }
+  __device__ __forceinline__ void one(const StencilArgs& A, uint64_t p, uint32_t* P, int bit) const {
+    if (p >= A.n_events) return;
+    if (RANGE) {
+      range(A.col[0][p], A.col[NCOL - 1][p], P, bit);
     } else {
-      for (int b = 0; b < kStPer + H; b++) {
-        const int64_t p = (int64_t)p0 - H + b;
-        if (p < 0 || (uint64_t)p >= A.n_events) continue;
-        valid |= 1u << b;
-        EvalIn in;
-        in.cols = &A.cols;
-        in.ftype = A.q->field_type;
-        in.ts = A.ts;
-        in.pos = (uint64_t)p;
-        in.W = nullptr;
-        in.wnull = 0;
-        in.curr = 0;
-        in.curr_null = true;
-        for (int s = 0; s < M; s++) {
-          bool rn;
-          int ee = 0;
-          const bool ok = interp(A.code, A.prog[s], in, &rn, &ee) != 0;  // total: never throws
-          P[s] |= (ok ? 1u : 0u) << b;
-        }
+      EvalIn in{&A.cols, A.q->field_type, A.ts, p, nullptr, 0, 0, true};
+      for (int s = 0; s < M; s++) {
+        bool rn;
+        int ee = 0;
+        if (interp(A.code, A.prog[s], in, &rn, &ee) != 0) P[s] |= 1u << bit;  // total: never throws
       }
     }
   }
-  // a key start strictly inside a window kills it: the window ending at bit e covers bits
-  // e-H..e, so a start at bit d kills the windows ending at d .. d+H-1.
-  uint32_t kill = 0;
-  uint32_t kb = 0;  // index of the last key start <= the thread's first window event
+};
+
+template <int M, bool RANGE, int NCOL>
+__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
+  constexpr int H = M - 1;  // events a window reaches back
+  __shared__ uint32_t s_cnt[kStThreads / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
+  const StEval<M, RANGE, NCOL> ev(A);
+  // carries: nibbles of the 8 events before the step (c1: -4..-1, c2: -8..-5), wave-uniform
+  uint32_t c1[M], c2[M];
+  uint32_t bc1 = 0, bc2 = 0;
   {
-    const int64_t lo = (int64_t)p0 - H - rel0;  // bit 0 of this thread, relative to rel0
-    uint32_t a = 0, b = nb;                     // upper_bound(lo) - 1
-    while (a < b) {
-      const uint32_t mid = (a + b) >> 1;
-      if ((int64_t)s_bnd[mid] <= lo) a = mid + 1;
-      else b = mid;
-    }
-    kb = a > 0 ? a - 1 : 0;
-    for (uint32_t i = a; i < nb; i++) {
-      const int64_t d = (int64_t)s_bnd[i] - lo;
-      if (d >= kStPer + H) break;
+    uint32_t P[M];
 #pragma unroll
-      for (int x = 0; x < H; x++) kill |= (1u << d) << x;
+    for (int s = 0; s < M; s++) P[s] = 0;
+    if (H > 0 && lane < 8 && wbase >= (uint64_t)(8 - lane)) ev.one(A, wbase - 8 + lane, P, 0);
+#pragma unroll
+    for (int s = 0; s < M; s++) {
+      const uint64_t b = __ballot(P[s] & 1u);
+      c2[s] = (uint32_t)b & 0xF;
+      c1[s] = (uint32_t)(b >> 4) & 0xF;
+    }
+    if (H > 0 && wbase >= 8) {  // key-start bits of events wbase-8 .. wbase-1 (wbase % 64 == 0)
+      const uint64_t w = A.bnd[wbase / 64 - 1];
+      bc2 = (uint32_t)(w >> 56) & 0xF;
+      bc1 = (uint32_t)(w >> 60) & 0xF;
     }
   }
-  uint32_t match = valid;
+  uint32_t cnt = 0;
+#pragma unroll 4
+  for (int q = 0; q < kStSteps; q++) {
+    const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
+    uint32_t P[M];
 #pragma unroll
-  for (int x = 0; x < M; x++) match &= P[M - 1 - x] << x;  // stage M-1-x at offset -x
-  match &= ~kill;
-  match >>= H;  // bit i -> event p0 + i
-  if (p0 >= tile_hi) match = 0;
-  match &= (kStPer >= 32) ? 0xFFFFFFFFu : ((1u << kStPer) - 1);
-  const uint32_t cnt = __popc(match);
+    for (int s = 0; s < M; s++) P[s] = 0;
+    if (RANGE && A.aligned && e0 + 4 <= A.n_events) {
+      const v4i x = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0));
+      v4i y = x;
+      if (NCOL > 1) y = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0));
+      ev.range(x.x, y.x, P, 0);
+      ev.range(x.y, y.y, P, 1);
+      ev.range(x.z, y.z, P, 2);
+      ev.range(x.w, y.w, P, 3);
+    } else if (e0 < A.n_events) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) ev.one(A, e0 + i, P, i);
+    }
+    uint32_t B = 0;
+    if (H > 0 && e0 < A.n_events) B = (uint32_t)(A.bnd[e0 / 64] >> (e0 % 64)) & 0xF;
+    // 12-bit windows: [11:8] this nibble, [7:4] the 4 events before, [3:0] the 4 before that
+    uint32_t match = 0xF;
+#pragma unroll
+    for (int s = 0; s < M; s++) {
+      uint32_t w = P[s] << 8;
+      if (H > 0) {
+        const uint32_t u1 = __shfl_up(P[s], 1, 64), u2 = __shfl_up(P[s], 2, 64);
+        const uint32_t p1 = lane >= 1 ? u1 : c1[s];
+        const uint32_t p2 = lane >= 2 ? u2 : (lane == 1 ? c1[s] : c2[s]);
+        w |= (p1 << 4) | p2;
+        c2[s] = __shfl(P[s], 62, 64);
+        c1[s] = __shfl(P[s], 63, 64);
+      }
+      // stage s sits at offset -(M-1-s) from the window's last event
+      match &= w >> (8 - (M - 1 - s));
+    }
+    if (H > 0) {
+      const uint32_t u1 = __shfl_up(B, 1, 64), u2 = __shfl_up(B, 2, 64);
+      const uint32_t b1 = lane >= 1 ? u1 : bc1;
+      const uint32_t b2 = lane >= 2 ? u2 : (lane == 1 ? bc1 : bc2);
+      const uint32_t bw = (B << 8) | (b1 << 4) | b2;
+      // a key start at any of the window's last M-1 events (not its first) kills it
+      uint32_t sm = 0;
+#pragma unroll
+      for (int x = 0; x < H; x++) sm |= bw << x;
+      match &= ~(sm >> 8);
+      bc2 = __shfl(B, 62, 64);
+      bc1 = __shfl(B, 63, 64);
+    }
+    match &= 0xF;
+    if (e0 + 4 > A.n_events) match &= e0 >= A.n_events ? 0u : ((1u << (A.n_events - e0)) - 1);
+    cnt += __popc(match);
+    // 16 lanes -> one 64-bit mask word
+    uint64_t word = (uint64_t)match << (4 * (lane & 15));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) word |= __shfl_xor(word, o, 64);
+    if ((lane & 15) == 0 && e0 < A.n_events) A.mask[e0 / 64] = word;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
+  if (lane == 0) s_cnt[wv] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) A.tile_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
 
-  // block exclusive scan of counts
-  uint32_t incl = cnt;
+// exclusive scan of the tile counts (one block; ~n_tiles/1024 sequential per thread)
+__global__ void __launch_bounds__(1024) stencil_scan(const uint32_t* cnt, uint64_t n, uint64_t* off, uint64_t* total) {
+  __shared__ uint64_t s[1024];
+  const uint64_t per = (n + 1023) / 1024;
+  const uint64_t a = threadIdx.x * per, b = (a + per < n) ? a + per : n;
+  uint64_t sum = 0;
+  for (uint64_t i = a; i < b; i++) sum += cnt[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint64_t y = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint64_t acc = s[threadIdx.x] - sum;
+  for (uint64_t i = a; i < b; i++) {
+    off[i] = acc;
+    acc += cnt[i];
+  }
+  if (threadIdx.x == 1023) *total = s[1023];
+}
+
+template <int M>
+__global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
+  __shared__ uint32_t s_wsum[kStThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
+  uint64_t match = 0, B = 0;
+  if (p0 < A.n_events) {
+    match = A.mask[p0 / 64];
+    B = A.bnd[p0 / 64];
+  }
+  const uint64_t Bk = (tid == 0) ? (B & ~1ull) : B;  // key starts after the tile's first event
+  const uint32_t cnt = (uint32_t)__popcll(match), bc = (uint32_t)__popcll(Bk);
+  // block exclusive scan of (matches, key starts), packed 16|16 (each <= 16384 per tile)
+  const uint32_t packed = (cnt << 16) | bc;
+  uint32_t incl = packed;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(incl, o, 64);
@@ -220,67 +294,26 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
   }
   if (lane == 63) s_wsum[wv] = incl;
   __syncthreads();
-  uint32_t woff = 0, agg = 0;
-  for (int w = 0; w < kStThreads / 64; w++) {
-    if (w < wv) woff += s_wsum[w];
-    agg += s_wsum[w];
-  }
-  // decoupled look-back for the tile's global offset, one wavefront reading 64 predecessor
-  // status granules per step: it stops at the nearest inclusive prefix and sums the
-  // aggregates in between, spinning only while a nearer predecessor has not published
-  if (wv == 0) {
-    unsigned long long excl = 0;
-    if (lane == 0)
-      __hip_atomic_store(&A.status[t], ((t == 0 ? 2ull : 1ull) << 62) | agg, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    if (t > 0) {
-      int64_t base = (int64_t)t - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t idx = base - lane;
-        const unsigned long long s =
-            idx >= 0 ? __hip_atomic_load(&A.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : (2ull << 62);  // before tile 0: inclusive prefix 0
-        const uint32_t flag = (uint32_t)(s >> 62);
-        const uint64_t inc = __ballot(flag == 2), zero = __ballot(flag == 0);
-        const int first = inc ? __builtin_ctzll(inc) : 64;
-        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);  // lanes 0..first
-        if (zero & upto) {
-          // predecessors took their tickets earlier, so they are resident and will publish;
-          // the bound only turns a bug into a reported error instead of a hang
-          if (++spins > (1u << 22)) {
-            if (lane == 0) atomicOr(A.overflow, 2u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        unsigned long long v = ((upto >> lane) & 1) ? (s & ((1ull << 62) - 1)) : 0;
+  uint32_t woff = 0;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-        excl += __shfl(v, 0, 64);
-        if (first < 64) break;
-        base -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&A.status[t], (2ull << 62) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      if (t == n_tiles - 1) *A.total = excl + agg;
-    }
-  }
-  __syncthreads();
-  uint64_t o = s_excl + woff + (incl - cnt);
-  unsigned long long dsum = 0;
+  for (int w = 0; w < kStThreads / 64; w++)
+    if (w < wv) woff += s_wsum[w];
+  const uint32_t excl = woff + incl - packed;
+  uint64_t o = A.tile_off[t] + (excl >> 16);
+  const uint32_t rank0 = A.tile_rank[t] + (excl & 0xFFFF);
+  uint32_t cur_rank = 0xFFFFFFFFu, key = 0;
+  uint64_t kstart = 0;
   while (match) {
-    const int i = __builtin_ctz(match);
+    const int i = __builtin_ctzll(match);
     match &= match - 1;
     const uint64_t p = p0 + i;
-    const int64_t pr = (int64_t)p - rel0;
-    while (kb + 1 < nb && (int64_t)s_bnd[kb + 1] <= pr) kb++;
-    const uint32_t key = s_bkey[kb];
-    const uint32_t seq = (uint32_t)(p - A.key_off[key]);
+    const uint32_t rk = rank0 + (uint32_t)__popcll(Bk & (i == 63 ? ~0ull : ((2ull << i) - 1)));
+    if (rk != cur_rank) {
+      cur_rank = rk;
+      key = A.nz_key[rk];
+      kstart = A.key_off[key];
+    }
+    const uint32_t seq = (uint32_t)(p - kstart);
     if (o < A.out_cap) {
       A.m_key[o] = key;
 #pragma unroll
@@ -288,42 +321,37 @@ __global__ void __launch_bounds__(kStThreads) stencil_kernel(StencilArgs A) {
     } else {
       atomicOr(A.overflow, 1u);
     }
-    uint64_t h = mix64s(0x9E3779B97F4A7C15ull ^ ((uint64_t)key << 32) ^ seq);
-#pragma unroll
-    for (int x = 0; x < M; x++) h = mix64s(h ^ (((uint64_t)A.stage_name[x] << 32) | (seq - x)));
-    dsum += h;
     o++;
-  }
-  // digest: wave reduce then one atomic per block
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dsum += __shfl_down(dsum, off, 64);
-  if (lane == 0) s_dig[wv] = dsum;
-  __syncthreads();
-  if (tid == 0) {
-    unsigned long long d = 0;
-    for (int w = 0; w < kStThreads / 64; w++) d += s_dig[w];
-    if (d) atomicAdd(A.digest, d);
   }
 }
 
-hipError_t launch_tile_first_key(const uint64_t* key_off, uint64_t n_keys, uint32_t* tile_key, uint64_t n_events,
-                                 hipStream_t st) {
+// ---------------------------------------------------------------- host launchers
+hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* rank,
+                            uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd, uint32_t* tile_rank,
+                            hipStream_t st) {
   const uint64_t n_tiles = (n_events + kStTile - 1) / kStTile;
   if (n_keys == 0 || n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(tile_first_key, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys,
-                     tile_key, n_tiles);
+  const uint64_t nb = (n_keys + 1023) / 1024;
+  hipLaunchKernelGGL(nz_rank_blocks, dim3((uint32_t)nb), dim3(1024), 0, st, key_off, n_keys, rank, bsum);
+  hipLaunchKernelGGL(nz_rank_top, dim3(1), dim3(1024), 0, st, bsum, nb);
+  hipLaunchKernelGGL(key_index, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, rank, bsum,
+                     nz_key, bnd, tile_rank, n_tiles);
+  return hipGetLastError();
+}
+
+template <int M, bool RANGE, int NCOL>
+static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
+  hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
+  hipLaunchKernelGGL(stencil_scan, dim3(1), dim3(1024), 0, st, a.tile_cnt, n_tiles, a.tile_off, a.total);
+  hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }
 
 template <int M>
 static hipError_t launch_m(const StencilArgs& a, bool range, int ncol, uint64_t n_tiles, hipStream_t st) {
-  if (range && ncol == 1)
-    hipLaunchKernelGGL((stencil_kernel<M, true, 1>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
-  else if (range)
-    hipLaunchKernelGGL((stencil_kernel<M, true, 2>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
-  else
-    hipLaunchKernelGGL((stencil_kernel<M, false, 1>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
-  return hipGetLastError();
+  if (range && ncol == 1) return launch_one<M, true, 1>(a, n_tiles, st);
+  if (range) return launch_one<M, true, 2>(a, n_tiles, st);
+  return launch_one<M, false, 1>(a, n_tiles, st);
 }
 
 hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st) {

@@ -1,0 +1,40 @@
+// stencil_args.h — kernel arguments of the strict-contiguity stencil (stencil.hip).  Kept out
+// of kernel_args.h, which is embedded into every JIT compile (and its cache key).
+#pragma once
+#include "kernel_args.h"
+
+namespace cep {
+
+struct RangeStage {  // conjunction of lo <= col_c <= hi for c in {0, 1}
+  int64_t lo[2], hi[2];
+};
+
+struct StencilArgs {
+  uint64_t n_keys, n_events;
+  const uint64_t* key_off;
+  const uint64_t* bnd;       // bit p: a non-empty key starts at event p
+  const uint32_t* tile_rank; // rank (among non-empty keys) of the key holding each tile's first event
+  const uint32_t* nz_key;    // rank -> key id
+  const int32_t* col[2];     // range fast path: up to two int columns
+  RangeStage rs[8];
+  // generic path (interpreted predicates)
+  const DevQuery* q;
+  const uint32_t* code;
+  Cols cols;
+  const int64_t* ts;
+  uint16_t prog[8];
+  uint16_t stage_name[8];    // walk order: stage name of pair t (t = 0 is the final event)
+  bool aligned;              // col[] 16-B aligned: vector loads
+  // pass 1 -> pass 3
+  uint64_t* mask;            // bit i of word w: a match ends at event 64 w + i
+  uint32_t* tile_cnt;        // matches per tile (pass 1), exclusive offsets after the scan
+  uint64_t* tile_off;
+  // output
+  uint32_t* m_key;
+  uint32_t* p_seq;           // [n_matches * m]
+  uint64_t* total;           // number of matches (stencil_scan)
+  uint64_t out_cap;          // matches that fit the output arrays
+  uint32_t* overflow;
+};
+
+}  // namespace cep
