@@ -36,9 +36,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 class Dist:
-    """torch.distributed (nccl = RCCL over xGMI) when launched with WORLD_SIZE > 1."""
+    """torch.distributed when launched with WORLD_SIZE > 1: "nccl" (= RCCL over xGMI) on the
+    GPUs, "gloo" on the CPU (tests/test_distributed.py)."""
 
-    def __init__(self):
+    def __init__(self, backend=None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -47,28 +48,41 @@ class Dist:
             import torch
             import torch.distributed as dist
 
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl")
+            self.backend = backend or "nccl"
+            self.device = "cuda" if self.backend == "nccl" else "cpu"
+            if self.device == "cuda":
+                torch.cuda.set_device(self.local)
+            dist.init_process_group(self.backend)
             self.torch, self.dist = torch, dist
 
     def barrier(self):
         if self.torch:
             self.dist.barrier()
-            self.torch.cuda.synchronize()
+            if self.device == "cuda":
+                self.torch.cuda.synchronize()
 
     def gather(self, vals):
         """all-gather a small float64 vector from every rank -> [world, len]"""
         if not self.torch:
             return np.asarray([vals], dtype=np.float64)
-        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.device)
         out = [self.torch.zeros_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t)
         return np.stack([o.cpu().numpy() for o in out])
 
+    def sum_u64(self, v):
+        """wrapping 64-bit sum over ranks (checksums), via an all-gather of two 32-bit halves"""
+        if not self.torch:
+            return v % (1 << 64)
+        t = self.torch.tensor([v & 0xFFFFFFFF, v >> 32], dtype=self.torch.int64, device=self.device)
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return sum(int(o[0]) + (int(o[1]) << 32) for o in out) % (1 << 64)
+
     def min_i64(self, v):
         if not self.torch:
             return v
-        t = self.torch.tensor([v], dtype=self.torch.int64, device="cuda")
+        t = self.torch.tensor([v], dtype=self.torch.int64, device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return int(t.item())
 
@@ -184,7 +198,8 @@ def main():
     N._check(N.lib().cep_poll_matches(sess.h, 0, N.CEP_MEM_DEVICE, N.C.byref(m)))
     n_pairs = m.n_pairs
     wm = dist.min_i64(sess.watermark())
-    per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err), float(digest % (1 << 52))])
+    per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err)])
+    checksum = dist.sum_u64(digest)  # wrapping sum of the shards' checksums (shard-local key ids)
     tot_ev, tot_m = per[:, 0].sum(), per[:, 1].sum()
     t_max = per[:, 3].max()
 
@@ -215,6 +230,7 @@ def main():
                          "kernel": "cep_nfa_jit", "kernel_ms": kms, "compaction_ms": aux_ms,
                          "algorithmic_bytes": alg},
             "watermark": wm,
+            "checksum": f"{checksum:016x}",
         }
         if dist.world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.variant, args.cpu_threads, args.cpu_every)

@@ -179,3 +179,54 @@ def test_watermark():
     off = np.array([0, 3], np.uint64)
     s.push(off, [np.array([1, 2, 3], np.int32), np.array([1, 2, 3], np.int32)], ts=np.array([5, 9, 7]))
     assert s.watermark() == 9
+
+
+def test_cfg2_full_size_checksum():
+    """Config 2 at its BASELINE size (1e8 events over 1e4 keys, generated in HBM): the
+    stencil's match count and checksum equal the oracle's on the same stream."""
+    cfg = W.CONFIGS[2]
+    d = N.synth_stream("abc", cfg.seed, cfg.n_keys, cfg.mean_events)
+    q = N.Query(W.strict_abc_query().to_ir())
+    assert q.kind == N.CEP_KIND_STENCIL
+    s = N.Session(q)
+    s.push_device(d)
+    n, dig = s.digest(0)
+    off, cols = d.download()
+    r = oracle.run(q.ir, off, cols, threads=16)
+    emit_seq = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+    pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+    pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+    assert n == r["n_matches"] > 3_000_000
+    assert dig == W.match_digest(r["key"], emit_seq, r["pair_off"], pseq, r["pair_stage"])
+    # size-independent property: every match is 3 consecutive events of one key, A B C
+    m = s.matches(0)
+    seq = m["pair_seq"].reshape(-1, 3).astype(np.int64)
+    assert np.all(seq[:, 0] == seq[:, 1] + 1) and np.all(seq[:, 1] == seq[:, 2] + 1)
+    v = cols[0]
+    base = off[m["key"].astype(np.int64)].astype(np.int64)
+    assert np.all(v[base + seq[:, 2]] < 4) and np.all((v[base + seq[:, 1]] >= 4) & (v[base + seq[:, 1]] < 8))
+    assert np.all(v[base + seq[:, 0]] >= 8)
+
+
+@pytest.mark.parametrize("tier", TIERS)
+def test_capacity_retry_small_queue(tier):
+    """A 2-record run queue overflows on most keys; they are re-run with 8x, 64x, 512x
+    the queue and the result is still exact."""
+    cfg = W.SynthConfig("t", "stock", 300, 600, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    q = N.Query(ir)
+    s = N.Session(q, max_runs=2, tier=tier)
+    r = oracle.run(ir, off, cols, threads=8)
+    assert r["max_live_runs"] > 2
+    assert_parity(gpu_run(ir, off, cols, session=s), r, off)
+
+
+def test_pool_growth_tiny_pools():
+    """Node/predecessor/output pools sized far below need: keys that run out are retried
+    with grown pools (indices of the kept prefix stay valid)."""
+    cfg = W.SynthConfig("t", "stock", 500, 800, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    s = N.Session(N.Query(ir), pool_factor=0.001)
+    assert_parity(gpu_run(ir, off, cols, session=s), oracle.run(ir, off, cols, threads=8), off)
