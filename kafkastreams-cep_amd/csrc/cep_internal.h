@@ -34,6 +34,7 @@ struct KeyState;
 
 hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap);  // double-buffered run queues
+uint64_t walkq_size(uint64_t n_slots, uint32_t wcap);        // deferred-walk queues
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,

@@ -24,7 +24,9 @@ constexpr int kDeweyPairs = 6;     // RLE pairs per Dewey version (overflow -> C
 
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
 enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3 };
-enum KeyErr : int32_t { KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16 };
+// KE_CONFLICT: a deferred walk would have changed what the step saw (nfa_lane.h); internal,
+// the key is re-run with walks in place
+enum KeyErr : int32_t { KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16, KE_CONFLICT = 17 };
 
 constexpr uint16_t kProgTrue = 0xFFFF;
 
@@ -81,21 +83,26 @@ struct Rec {
 };
 
 // ---- buffer node (TimedKeyValue + its StackEventKey, nfa/buffer/impl/TimedKeyValue.java)
-struct Node {
+// Two 16-B quads, read and written as vectors: {event, refs, head, tail}, {same_next, meta, lk, -}
+struct alignas(16) Node {
   uint32_t event;      // sequence number within key
   int32_t refs;        // TimedKeyValue.refs
   uint32_t head, tail; // predecessor list (Pred indices), insertion order
   uint32_t same_next;  // next node created at the same event (lookup chain)
   uint32_t meta;       // [7:0] stage key, bit8 live, [31:16] live predecessor count
+  uint32_t lk;         // walks queued when put() last found this node live (deferred walks)
+  uint32_t pad;
 };
 
-// ---- predecessor pointer (TimedKeyValue.Pointer): (version, key|null)
-struct Pred {
+// ---- predecessor pointer (TimedKeyValue.Pointer): (version, key|null).  Four quads:
+// {prev, next, removed | pairs << 8, Dewey length}, then the Dewey (value, count) pairs,
+// two per quad (only quads holding live pairs are written or read)
+struct alignas(16) Pred {
   uint32_t prev;   // node index of the key, CEP_NONE = null key
   uint32_t next;   // next Pred of the node, CEP_NONE = end
-  uint32_t removed;
-  uint32_t pad;
-  Dewey ver;
+  uint32_t flags;  // bit0 removed, [15:8] Dewey pairs in use
+  uint32_t len;
+  uint32_t pair[2 * kDeweyPairs];  // v0, c0, v1, c1, ...
 };
 
 // ---- per-key state kept between kernel phases

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -507,12 +508,24 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "struct Fo {\n  int64_t v[F];\n  uint32_t nm;\n};\n";
   o += "struct Top {\n  uint32_t stage, event, ev_first;\n};\n";
   o += "struct Out {\n  int produced;\n  int same;  // slot of the output record that keeps the run's sequence id\n};\n\n";
-  o += "__device__ __forceinline__ void load_ev(Ev& ev, const NfaArgs& A, uint64_t pos) {\n";
-  for (uint32_t f = 0; f < d.n_fields; f++)
-    if (fields[f])
-      o += "  ev.f" + std::to_string(f) + " = ((const " + ctype(d.field_type[f]) + "*)A.cols.p[" + std::to_string(f) + "])[pos];\n";
-  o += ts ? "  ev.ts = A.ts ? A.ts[pos] : (int64_t)pos;\n" : "  ev.ts = 0;\n";
-  o += "}\n\n";
+  // the begin predicate's own columns (the quiet scan loads only these)
+  std::vector<bool> bfields(d.n_fields, false);
+  bool bts = false;
+  for (auto& pe : b.pending)
+    if (pe.stage == (int)d.begin_stage && pe.edge == 0) usesM(pe.m.get(), bfields, bts);
+  auto loader = [&](const char* name, const std::vector<bool>& use, bool uts) {
+    o += std::string("__device__ __forceinline__ void ") + name + "(Ev& ev, const NfaArgs& A, uint64_t pos) {\n";
+    for (uint32_t f = 0; f < d.n_fields; f++)
+      if (fields[f])
+        o += "  ev.f" + std::to_string(f) + " = " +
+             (use[f] ? "((const " + std::string(ctype(d.field_type[f])) + "*)A.cols.p[" + std::to_string(f) + "])[pos]"
+                     : std::string("0")) + ";\n";
+    o += uts ? "  ev.ts = A.ts ? A.ts[pos] : (int64_t)pos;\n" : "  ev.ts = 0;\n";
+    o += "}\n";
+  };
+  loader("ld_ev", fields, ts);
+  loader("ld_bev", bfields, bts);
+  o += "\n";
   // predicates, one per (stage, edge); folds one per (stage, aggregate)
   std::vector<std::vector<std::string>> predName(d.n_stages, std::vector<std::string>(3));
   for (auto& pe : b.pending) {
@@ -552,8 +565,13 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   const bool quiet = bs.n_edges == 1 && bs.e[0].op == OP_BEGIN;
   o += "  static constexpr bool quiet = " + std::string(quiet ? "true" : "false") + ";\n";
   o += "  static constexpr bool kBeginReg = quiet;\n";
+  bool fold32 = true;  // every state a Java int: one word per fold slot in the run record
+  for (uint32_t i = 0; i < d.n_states; i++) fold32 = fold32 && d.state_type[i] == 1;
+  o += "  static constexpr bool kFold32 = " + std::string(fold32 ? "true" : "false") + ";\n";
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
+  o += "  typedef Ev EvT;\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
+  o += "  __device__ __forceinline__ void load_ev(Ev& e, uint64_t pos) const { ld_ev(e, A, pos); }\n";
   o += "  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {\n    if (sw & kRecEps) return (sw >> 8) & 0xFF;\n    switch (sw & 0xFF) {\n";
   for (uint32_t s = 0; s < d.n_stages; s++) o += "      case " + std::to_string(s) + ": return " + std::to_string(d.st[s].sk) + ";\n";
   o += "    }\n    return 0;\n  }\n";
@@ -561,11 +579,26 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   for (uint32_t k = 0; k < d.n_sk; k++) o += "      case " + std::to_string(k) + ": return " + std::to_string(d.sk_name[k]) + ";\n";
   o += "    }\n    return 0;\n  }\n";
   o += "  template <class LT>\n  __device__ __forceinline__ bool begin_pred(LT& L) {\n";
-  if (quiet && !predName[d.begin_stage][0].empty()) {
-    o += "    Ev ev;\n    load_ev(ev, A, L.base + L.j);\n    Fo w;\n    w.nm = (1u << F) - 1;\n    int err = 0;\n";
-    o += "    const bool r = " + predName[d.begin_stage][0] + "(ev, w, err);\n    if (err) L.err = err;\n    return r;\n";
+  const bool bpred = quiet && !predName[d.begin_stage][0].empty();
+  if (bpred) {
+    o += "    Fo w;\n    w.nm = (1u << F) - 1;\n    int err = 0;\n";
+    o += "    const bool r = " + predName[d.begin_stage][0] + "(L.ev, w, err);\n    if (err) L.err = err;\n    return r;\n";
   } else {
     o += "    return true;\n";
+  }
+  o += "  }\n";
+  // quiet scan: the chunk's loads issued together, then the predicate in event order (a
+  // later event's result or exception is never used past the first hit)
+  o += "  template <class LT>\n  __device__ __forceinline__ uint32_t begin_scan(LT& L, uint32_t j0, uint32_t lim) {\n";
+  if (bpred) {
+    o += "    Ev e[kQuietChunk];\n";
+    o += "#pragma unroll\n    for (uint32_t i = 0; i < kQuietChunk; i++) ld_bev(e[i], A, L.base + (j0 + i < lim ? j0 + i : j0));\n";
+    o += "#pragma unroll\n    for (uint32_t i = 0; i < kQuietChunk; i++) {\n      if (j0 + i >= lim) break;\n";
+    o += "      Fo w;\n      w.nm = (1u << F) - 1;\n      int err = 0;\n";
+    o += "      const bool r = " + predName[d.begin_stage][0] + "(e[i], w, err);\n";
+    o += "      if (err) { L.err = err; return j0 + i; }\n      if (r) return j0 + i;\n    }\n    return lim;\n";
+  } else {
+    o += "    return j0;\n";
   }
   o += "  }\n";
   // stage functions in reverse creation order so that PROCEED targets are declared first:
@@ -650,7 +683,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   }
   // step: dispatch on the record's stage (epsilon -> its PROCEED target, real -> begin stage)
   o += "  template <class LT>\n  __device__ __forceinline__ int step(LT& L, const Rec<F>& c) {\n";
-  o += "    Ev ev;\n    load_ev(ev, A, L.base + L.j);\n    Fo w;\n";
+  o += "    const Ev& ev = L.ev;\n    Fo w;\n";
   o += "    for (int s = 0; s < F; s++) w.v[s] = c.fold[s];\n    w.nm = c.nullmask;\n";
   o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
@@ -671,7 +704,11 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = KE_CAPACITY; return -1; }\n";
   o += "      if (!L.readd_begin(c.stage & 0xFF, v)) return -1;\n";
   o += "      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
-  o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256) cep_nfa_jit(NfaArgs A) {\n";
+  // occupancy knob for tuning runs: $CEP_JIT_WAVES = minimum waves per SIMD (0: compiler's choice)
+  std::string occ;
+  if (const char* wv = std::getenv("CEP_JIT_WAVES"))
+    if (std::atoi(wv) > 0) occ = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(wv)) + ")))";
+  o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256)" + occ + " cep_nfa_jit(NfaArgs A) {\n";
   o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n}  // namespace cep\n";
   return o;
 }

@@ -26,6 +26,9 @@ struct NfaArgs {
   const int64_t* ts;
   void* rings;               // Rec<F>[n_slots * rcap]
   uint32_t rcap;
+  void* walks;               // deferred-walk queues, wcap per slot (nfa_lane.h)
+  uint32_t wcap;
+  uint32_t defer;            // 1: queue buffer walks and drain them wave-wide; 0: walk in place
   const uint32_t* key_list;  // retry pass: slot i runs key key_list[i]; null = all keys
   uint32_t n_list;
   Node* nodes;

@@ -38,6 +38,8 @@ struct InterpQ {
   bool quiet;
   uint32_t begin_stage;
   static constexpr bool kBeginReg = false;  // quiet is only known at run time here
+  static constexpr bool kFold32 = false;     // fold slots hold any state type
+  struct EvT {};                             // the programs read the columns themselves
 
   __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {
     begin_stage = q.begin_stage;
@@ -60,6 +62,18 @@ struct InterpQ {
     const int64_t r = interp(code, E.prog, in, &rn, &ee);
     if (ee) lane.err = ee;
     return r != 0;
+  }
+
+  __device__ __forceinline__ void load_ev(EvT&, uint64_t) const {}
+
+  template <class LaneT>
+  __device__ uint32_t begin_scan(LaneT& lane, uint32_t j0, uint32_t lim) {
+    for (uint32_t p = j0; p < lim; p++) {
+      lane.j = p;
+      const bool hit = begin_pred(lane);
+      if (lane.err || hit) return p;
+    }
+    return lim;
   }
 
   // NFA.matchPattern(ctx) :139-160.  Returns the number of records produced; -1 on error.
@@ -414,6 +428,8 @@ hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_le
     default: return launch_nfa_t<8>(a, nslots, code_len, st);
   }
 }
+
+uint64_t walkq_size(uint64_t n_slots, uint32_t wcap) { return walkq_bytes(n_slots, wcap); }
 
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap) {
   return ring_bytes(F <= 2 ? 2 : (F <= 4 ? 4 : 8), n_slots, rcap);

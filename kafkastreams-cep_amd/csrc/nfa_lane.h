@@ -10,13 +10,18 @@
 //   put / put(begin) / branch / peek(remove)               KVSharedVersionedBuffer :80-171
 //
 // Policy interface (Q):
+//   EvT                                      the event fields the query reads (registers)
+//   void load_ev(EvT&, uint64_t pos)         loads them for CSR position pos
 //   uint32_t stage_sk(uint32_t stage_word)   stage key of a record's stage (Stage.equals identity)
 //   uint16_t sk_name(uint32_t sk)            stage-name id of a stage key (output)
-//   int step(Lane&, const Rec<F>&)           NFA.matchPattern(ctx): records produced, -1 on error
+//   int step(Lane&, const Rec<F>&)           NFA.matchPattern(ctx) on L.ev: records produced, -1 on error
 //   bool quiet                               the begin stage has a single BEGIN edge
 //   uint32_t begin_stage                     its stage index
-//   bool begin_pred(Lane&)                   its predicate on event j with all-null folds
+//   bool begin_pred(Lane&)                   its predicate on L.ev with all-null folds
+//   uint32_t begin_scan(Lane&, j0, lim)      first position in [j0, lim) where begin_pred is
+//                                            true or throws (L.err set), else lim
 //   bool kBeginReg                           keep the begin run in registers (needs quiet)
+//   bool kFold32                             every fold state is a 32-bit int
 //
 // Run queue layout.  The queue a key holds between events is double-buffered: the records
 // of event j are read from one half (slots 0..count-1) and the records they produce are
@@ -25,11 +30,30 @@
 // same (half, slot, quad) - the common case, the queue loop runs in lockstep - form one
 // fully coalesced 1 KiB access.  A record is kQuads quads: header {stage | Dewey pairs << 24,
 // event, ev_first, Dewey length}, the Dewey (value, count) pairs two per quad (only quads
-// holding live pairs are read or written), then {nullmask, -, fold0, fold1, ...}.
+// holding live pairs are read or written), then {nullmask, -, fold0, fold1, ...} (64-bit
+// slots) or {nullmask, fold0, fold1, ...} when every fold state is an int (kFold32).
+// A record created at event j does not know the node chain of j until the event ends; it is
+// written with ev_first = kPending and resolved when it is next loaded (event j+1, or the
+// final-match pass of event j itself).
 //
 // When the begin stage has a single BEGIN edge (kBeginReg) the begin run, always the last
 // record of the queue (NFA.java:148-157 re-adds it after its own outputs), lives in
 // registers as its single Dewey digit: the ring holds live runs only.
+//
+// Deferred walks (A.defer).  The buffer walks - branch (refs++ along a path), removePattern
+// and match extraction (peek with remove) - are pointer chases of O(path) dependent loads.
+// Run in place, a lane walking stalls the 63 others.  Instead each walk is queued (in
+// order) and the wave drains all queues together in one loop where every lane advances its
+// own walk by one node per iteration, so the wave pays for the longest queue, not the sum.
+// This is exact because the per-event work between a walk and its deferred execution never
+// observes a walk's effects: walks change refcounts, predecessor lists and live bits of
+// nodes of events before the walk's own event; the step only appends to nodes of the
+// current event and reads older nodes through put()'s predecessor lookup, which checks the
+// live bit.  That one read is checked: every such lookup stamps the node with the number of
+// walks queued so far, and a walk that deletes a node stamped after it was queued (the
+// reference would have thrown "Cannot find predecessor event") reports KE_CONFLICT; the key
+// is then re-run with walks in place (session.cpp).  Errors keep their reference order: a
+// walk's exception precedes anything the step did after queueing it.
 #pragma once
 #include "dewey.h"
 
@@ -37,54 +61,80 @@ namespace cep {
 
 constexpr uint32_t kNoSk = 0xFF;
 constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at the current event
-constexpr uint32_t kQuietChunk = 16;        // events a runs-free lane may skip per driver step
+constexpr uint32_t kQuietChunk = 16;        // events a runs-free lane scans per driver step
+constexpr uint32_t kWalkFlush = 8;          // a queue this long drains the wave's walk queues
+constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
+constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
 
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+// may_alias: quads of Node/Pred are also read and written field by field (Node::refs, ...);
+// without it TBAA lets the compiler reorder the two views of the same bytes
+typedef uint32_t v4u __attribute__((ext_vector_type(4), may_alias));
 
-template <int F>
+// W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
+template <int F, bool W32 = false>
 struct RecLayout {
   static constexpr int kDwQuads = (kDeweyPairs + 1) / 2;
-  static constexpr int kFoldQuads = (2 + 2 * F + 3) / 4;
+  static constexpr int kFoldQuads = W32 ? (1 + F + 3) / 4 : (2 + 2 * F + 3) / 4;
   static constexpr int kQuads = 1 + kDwQuads + kFoldQuads;
 };
 
-// bytes of double-buffered run queues for n_slots lanes of rcap records
+// bytes of double-buffered run queues for n_slots lanes of rcap records (64-bit folds: the
+// larger layout, so one allocation serves every query)
 __host__ __device__ inline uint64_t ring_bytes(int F, uint64_t n_slots, uint32_t rcap) {
   const int quads = 1 + (kDeweyPairs + 1) / 2 + (2 + 2 * F + 3) / 4;
   return ((n_slots + 63) / 64) * 64ull * 2ull * rcap * quads * 16ull;
 }
 
+// bytes of deferred-walk queues for n_slots lanes of wcap walks
+__host__ __device__ inline uint64_t walkq_bytes(uint64_t n_slots, uint32_t wcap) {
+  return ((n_slots + 63) / 64) * 64ull * wcap * kWalkQuads * 16ull;
+}
+
 template <int F, class Q>
 struct Lane {
-  using Lay = RecLayout<F>;
+  using Lay = RecLayout<F, Q::kFold32>;
+  using EvT = typename Q::EvT;
   static constexpr bool kBeginReg = Q::kBeginReg;
   const NfaArgs& A;
   Q& q;
   uint32_t key;
   uint64_t base;
-  uint32_t j = 0;  // current event (sequence number within the key)
-  v4u* rb;         // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
+  uint32_t n_ev = 0;  // events of the key
+  uint32_t j = 0;     // current event (sequence number within the key)
+  EvT ev;             // fields of event ev_pos
+  uint32_t ev_pos = CEP_NONE;
+  v4u* rb;  // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
+  v4u* wb;  // this lane's walk queue, slot 0 quad 0 (stride 64 quads)
   uint32_t half = 0, count = 0, ocount = 0;  // input half, its records, records written
   uint32_t bdig = 1;                         // kBeginReg: the begin run's version "bdig"
-  uint32_t pending = 0, n_final = 0;  // records of this event awaiting ev_first / finals queued
+  uint32_t n_final = 0;                      // finals queued at this event
   uint32_t ncur = 0, nend = 0, pcur = 0, pend = 0;
   uint32_t ochunk = CEP_NONE, opos = 0;
   uint32_t cur_first = CEP_NONE;  // node chain of event j
   int err = KE_OK;
+  uint32_t err_seq = 0;
   uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
+  // deferred walks
+  uint32_t wq_n = 0;  // queued
+  uint32_t opc = 0;   // walks queued since the key started (walk ids)
+  uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
 
   __device__ Lane(const NfaArgs& a, Q& qq) : A(a), q(qq) {}
 
   __device__ __forceinline__ v4u* QP(uint32_t h, uint32_t slot, int quad) const {
     return rb + ((uint64_t)(h * A.rcap + slot) * Lay::kQuads + quad) * 64;
   }
+  __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
+    return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
+  }
 
   // ---------------------------------------------------------------- records
-  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r) const {
+  // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
+  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf) const {
     const v4u hd = *QP(h, slot, 0);
     r.stage = hd.x & 0x00FFFFFFu;
     r.event = hd.y;
-    r.ev_first = hd.z;
+    r.ev_first = hd.z == kPending ? pf : hd.z;
     r.ver.n = hd.x >> 24;
     r.ver.len = hd.w;
 #pragma unroll
@@ -109,7 +159,8 @@ struct Lane {
     }
     r.nullmask = w[0];
 #pragma unroll
-    for (int s = 0; s < F; s++) r.fold[s] = (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
+    for (int s = 0; s < F; s++)
+      r.fold[s] = Q::kFold32 ? (int64_t)(int32_t)w[1 + s] : (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
   }
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
@@ -131,8 +182,12 @@ struct Lane {
     w[0] = nm;
 #pragma unroll
     for (int s = 0; s < F; s++) {
-      w[2 + 2 * s] = (uint32_t)(uint64_t)v[s];
-      w[3 + 2 * s] = (uint32_t)((uint64_t)v[s] >> 32);
+      if (Q::kFold32) {
+        w[1 + s] = (uint32_t)(uint64_t)v[s];
+      } else {
+        w[2 + 2 * s] = (uint32_t)(uint64_t)v[s];
+        w[3 + 2 * s] = (uint32_t)((uint64_t)v[s] >> 32);
+      }
     }
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++)
@@ -146,18 +201,14 @@ struct Lane {
 
   // Appends an output record (header + version) and returns its slot, -1 when the queue is
   // full.  ev_first of a record whose event is the current one is only known once the
-  // event's nodes exist: marked pending, patched after the event.  Folds: set_folds.
+  // event's nodes exist: kPending, resolved at its next load.  Folds: set_folds.
   __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver) {
     if (ocount >= A.rcap) {
       err = KE_CAPACITY;
       return -1;
     }
     const uint32_t slot = ocount++;
-    uint32_t ef = ev_first;
-    if (event == j && ev_first == CEP_NONE) {
-      ef = kPending;
-      pending++;
-    }
+    const uint32_t ef = (event == j && ev_first == CEP_NONE) ? kPending : ev_first;
     store_head(half ^ 1u, slot, stage, event, ef, ver);
     if (stage & kRecFinal) n_final++;
     return (int)slot;
@@ -183,42 +234,56 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- buffer nodes
+  __device__ __forceinline__ v4u* NQ(uint32_t i, int k) const { return reinterpret_cast<v4u*>(A.nodes + i) + k; }
+  __device__ __forceinline__ v4u* PQ(uint32_t i, int k) const { return reinterpret_cast<v4u*>(A.preds + i) + k; }
+
+  // node (sk, event of the chain); CEP_NONE when absent or deleted.
+  // Pool reads whose result feeds the next address of a loop (chains, predecessor lists,
+  // walks) are written field by field: the same reads as one 16-B vector load were seen
+  // to loop forever on gfx950 (the loop-carried value never advanced); stores stay vectors.
   __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
     for (uint32_t i = first; i != CEP_NONE;) {
       const Node& n = A.nodes[i];
-      if ((n.meta & 0xFF) == sk) return (n.meta & 0x100) ? i : CEP_NONE;
-      i = n.same_next;
+      const uint32_t meta = n.meta, nx = n.same_next;
+      if ((meta & 0xFF) == sk) return (meta & 0x100) ? i : CEP_NONE;
+      i = nx;
     }
     return CEP_NONE;
   }
 
-  __device__ __forceinline__ uint32_t new_node(uint32_t sk) {
-    const uint32_t i = pool_take(A.node_pool, ncur, nend);
-    if (i == CEP_NONE) {
-      err = KE_CAPACITY;
-      return CEP_NONE;
-    }
-    Node& n = A.nodes[i];
-    n.event = j;
-    n.refs = 1;
-    n.head = n.tail = CEP_NONE;
-    n.same_next = cur_first;
-    n.meta = sk | 0x100;
-    cur_first = i;
-    return i;
+  __device__ __forceinline__ void write_pred(uint32_t p, uint32_t prev, const Dewey& v0) {
+    const Dewey v = dw_pin(v0);
+    *PQ(p, 0) = v4u{prev, CEP_NONE, v.n << 8, v.len};
+#pragma unroll
+    for (int k = 0; k < (kDeweyPairs + 1) / 2; k++)
+      if ((uint32_t)(2 * k) < v.n)
+        *PQ(p, 1 + k) = v4u{(uint32_t)v.v[2 * k], v.c[2 * k],
+                            2 * k + 1 < kDeweyPairs ? (uint32_t)v.v[2 * k + 1] : 0u,
+                            2 * k + 1 < kDeweyPairs ? v.c[2 * k + 1] : 0u};
   }
 
+  // a new node at event j holding one predecessor (prev, v): both written as whole quads
+  __device__ __forceinline__ void new_node(uint32_t sk, uint32_t prev, const Dewey& v) {
+    const uint32_t i = pool_take(A.node_pool, ncur, nend);
+    const uint32_t p = i == CEP_NONE ? CEP_NONE : pool_take(A.pred_pool, pcur, pend);
+    if (p == CEP_NONE) {
+      err = KE_CAPACITY;
+      return;
+    }
+    write_pred(p, prev, v);
+    *NQ(i, 0) = v4u{j, 1u, p, p};
+    *NQ(i, 1) = v4u{cur_first, sk | 0x100u | (1u << 16), 0u, 0u};
+    cur_first = i;
+  }
+
+  // appends (prev, v) to an existing node of event j
   __device__ __forceinline__ void append_pred(uint32_t node, uint32_t prev, const Dewey& v) {
     const uint32_t p = pool_take(A.pred_pool, pcur, pend);
     if (p == CEP_NONE) {
       err = KE_CAPACITY;
       return;
     }
-    Pred& e = A.preds[p];
-    e.prev = prev;
-    e.next = CEP_NONE;
-    e.removed = 0;
-    dw_store(e.ver, v);
+    write_pred(p, prev, v);
     Node& n = A.nodes[node];
     if (n.head == CEP_NONE) n.head = p;
     else A.preds[n.tail].next = p;
@@ -228,17 +293,22 @@ struct Lane {
 
   // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
   __device__ __forceinline__ void put_begin(uint32_t sk, const Dewey& v) {
-    uint32_t c = lookup(sk, cur_first);
+    const uint32_t c = lookup(sk, cur_first);
     if (c == CEP_NONE) {
-      c = new_node(sk);
-      if (err) return;
-    } else {
-      Node& n = A.nodes[c];
-      n.refs = 1;
-      n.head = n.tail = CEP_NONE;
-      n.meta = sk | 0x100;
+      new_node(sk, CEP_NONE, v);
+      return;
     }
-    append_pred(c, CEP_NONE, v);
+    const uint32_t p = pool_take(A.pred_pool, pcur, pend);  // a new TimedKeyValue, one pointer
+    if (p == CEP_NONE) {
+      err = KE_CAPACITY;
+      return;
+    }
+    write_pred(p, CEP_NONE, v);
+    Node& n = A.nodes[c];
+    n.refs = 1;
+    n.head = p;
+    n.tail = p;
+    n.meta = sk | 0x100u | (1u << 16);
   }
 
   // put(curr, currEvent, prev, prevEvent, version)  :80-97;  prev_sk == kNoSk: put(begin)
@@ -257,45 +327,43 @@ struct Lane {
       err = KE_ILLEGAL_STATE;
       return;
     }
-    uint32_t c = lookup(sk, cur_first);
-    if (c == CEP_NONE) {
-      c = new_node(sk);
-      if (err) return;
-    }
-    append_pred(c, p, v);
+    if (A.defer) A.nodes[p].lk = opc;  // found live after `opc` queued walks (conflict check)
+    const uint32_t c = lookup(sk, cur_first);
+    if (c == CEP_NONE) new_node(sk, p, v);
+    else append_pred(c, p, v);
   }
 
-  // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92
-  __device__ __forceinline__ uint32_t first_compat(uint32_t node, const Dewey& walker) {
-    for (uint32_t p = A.nodes[node].head; p != CEP_NONE; p = A.preds[p].next) {
-      const Pred& e = A.preds[p];
-      if (e.removed) continue;
-      if (dw_compatible(walker, e.ver)) return p;
+  // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92, from the node's list head:
+  // the first live pointer whose version the walker is compatible with; its key and version
+  // come back in prev / ver
+  __device__ __forceinline__ uint32_t first_compat(uint32_t head, const Dewey& walker, uint32_t& prev, Dewey& ver) {
+    for (uint32_t p = head; p != CEP_NONE;) {
+      const Pred& e0 = A.preds[p];
+      const uint32_t fl = e0.flags, nxt = e0.next;
+      if (!(fl & 1u)) {
+        Dewey e;
+        e.n = (fl >> 8) & 0xFF;
+        e.len = e0.len;
+#pragma unroll
+        for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
+          v4u d = {0, 0, 0, 0};
+          if ((uint32_t)(2 * k) < e.n) d = *PQ(p, 1 + k);
+          e.v[2 * k] = (int32_t)d.x;
+          e.c[2 * k] = d.y;
+          if (2 * k + 1 < kDeweyPairs) {
+            e.v[2 * k + 1] = (int32_t)d.z;
+            e.c[2 * k + 1] = d.w;
+          }
+        }
+        if (dw_compatible(walker, e)) {
+          prev = e0.prev;
+          ver = dw_pin(e);
+          return p;
+        }
+      }
+      p = nxt;
     }
     return CEP_NONE;
-  }
-
-  // branch  :99-110
-  __device__ __forceinline__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v) {
-    if (ev == CEP_NONE) {
-      err = KE_NPE;
-      return;
-    }
-    uint32_t s = lookup(sk, first);
-    Dewey w = dw_pin(v);
-    for (;;) {
-      if (s == CEP_NONE || !(A.nodes[s].meta & 0x100)) {
-        err = KE_NPE;
-        return;
-      }
-      A.nodes[s].refs += 1;
-      const uint32_t p = first_compat(s, w);
-      if (p == CEP_NONE) return;
-      const uint32_t nx = A.preds[p].prev;
-      if (nx == CEP_NONE) return;
-      w = dw_pin(A.preds[p].ver);  // a value, not a pointer into the pool
-      s = nx;
-    }
   }
 
   // ---------------------------------------------------------------- output stream
@@ -316,69 +384,202 @@ struct Lane {
     return a;
   }
 
-  // peek(stage, event, version, remove=true)  :143-171; emit = match construction
-  __device__ __forceinline__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit) {
-    if (ev == CEP_NONE) {
-      err = KE_NPE;
+  // ---------------------------------------------------------------- walks
+  // branch  KVSharedVersionedBuffer.java:99-110;  peek(remove=true)  :143-171 (emit: the
+  // match construction's Sequence).  In place when !A.defer, else queued (see the header).
+  __device__ __forceinline__ void walk(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v0) {
+    if (!A.defer) {
+      walk_now(flags, sk, ev, first, v0, j);
       return;
     }
-    uint32_t s = lookup(sk, first);
-    Dewey w = dw_pin(v);
-    uint64_t npair_addr = 0;
-    uint32_t np = 0;
-    if (emit) {
-      out_put(j);
-      npair_addr = out_put(0);
-      if (err) return;
+    if (wq_n >= A.wcap) {  // more walks in one event than the queue holds: re-run in place
+      err = KE_CAPACITY;
+      return;
     }
-    for (;;) {
-      if (s == CEP_NONE) {
-        err = KE_NPE;
-        return;
-      }
-      Node& n = A.nodes[s];
-      const uint32_t meta = n.meta;
-      if (!(meta & 0x100)) {
-        err = KE_NPE;
-        return;
-      }
-      const int32_t left = n.refs == 0 ? 0 : n.refs - 1;
+    const Dewey v = dw_pin(v0);
+    *WQ(wq_n, 0) = v4u{sk | (flags << 8) | (v.n << 24), ev, first, v.len};
+#pragma unroll
+    for (int k = 0; k < (kDeweyPairs + 1) / 2; k++)
+      if ((uint32_t)(2 * k) < v.n)
+        *WQ(wq_n, 1 + k) = v4u{(uint32_t)v.v[2 * k], v.c[2 * k],
+                               2 * k + 1 < kDeweyPairs ? (uint32_t)v.v[2 * k + 1] : 0u,
+                               2 * k + 1 < kDeweyPairs ? v.c[2 * k + 1] : 0u};
+    reinterpret_cast<uint32_t*>(WQ(wq_n, kWalkQuads - 1))[0] = j;
+    wq_n++;
+    opc++;
+  }
+  __device__ __forceinline__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v) {
+    walk(kWalkBranch, sk, ev, first, v);
+  }
+  __device__ __forceinline__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit) {
+    walk(emit ? kWalkEmit : 0u, sk, ev, first, v);
+  }
+
+  // a walk of event t threw: nothing of event t is forwarded, the key stops at t
+  __device__ __forceinline__ void walk_fail(int code, uint32_t t) {
+    err = code;
+    err_seq = t;
+    n_matches = wm0;
+    n_pairs = wp0;
+  }
+
+  __device__ __forceinline__ void walk_begin(uint32_t t) {
+    if (t != wt_last) {
+      wt_last = t;
+      wm0 = n_matches;
+      wp0 = n_pairs;
+    }
+  }
+
+  // One node of a walk at node s with walker version w.  Returns false when the walk ends
+  // (or fails); s/w advance to the next node otherwise.  `wid`: the walk's id (deferred).
+  __device__ __forceinline__ bool walk_node(uint32_t flags, uint32_t& s, Dewey& w, uint32_t t, uint32_t wid,
+                                            uint32_t& np) {
+    if (s == CEP_NONE) {
+      walk_fail(KE_NPE, t);
+      return false;
+    }
+    Node& n = A.nodes[s];
+    const uint32_t ev_s = n.event, head = n.head, lk = n.lk;
+    uint32_t meta = n.meta;
+    if (!(meta & 0x100)) {
+      walk_fail(KE_NPE, t);
+      return false;
+    }
+    const int32_t refs = n.refs;
+    int32_t left = 1;
+    if (flags & kWalkBranch) {
+      n.refs = refs + 1;
+    } else {
+      left = refs == 0 ? 0 : refs - 1;
       n.refs = left;
-      if (left == 0 && (meta >> 16) <= 1) n.meta = meta & ~0x100u;  // store.delete
-      if (emit) {
-        out_put(n.event);
+      if (left == 0 && (meta >> 16) <= 1) {  // store.delete
+        if (A.defer && lk > wid) {          // a put() after this walk found the node live
+          walk_fail(KE_CONFLICT, t);
+          return false;
+        }
+        meta &= ~0x100u;
+        n.meta = meta;
+      }
+      if (flags & kWalkEmit) {
+        out_put(ev_s);
         out_put(q.sk_name(meta & 0xFF));
         np++;
-        if (err) return;
+        if (err) {
+          walk_fail(err, t);
+          return false;
+        }
       }
-      const uint32_t p = first_compat(s, w);
-      if (p == CEP_NONE) break;
-      if (left == 0) {  // removePredecessor(pointer)
-        A.preds[p].removed = 1;
-        n.meta -= 1u << 16;
-      }
-      const uint32_t nx = A.preds[p].prev;
-      if (nx == CEP_NONE) break;
-      w = dw_pin(A.preds[p].ver);  // a value, not a pointer into the pool
-      s = nx;
     }
-    if (emit) {
-      A.out[npair_addr] = np;
+    uint32_t nx = CEP_NONE;
+    Dewey nv;
+    const uint32_t p = first_compat(head, w, nx, nv);
+    if (p == CEP_NONE) return false;
+    if (left == 0) {  // removePredecessor(pointer)
+      A.preds[p].flags |= 1u;
+      n.meta = meta - (1u << 16);
+    }
+    if (nx == CEP_NONE) return false;
+    w = nv;  // a value, not a pointer into the pool
+    s = nx;
+    return true;
+  }
+
+  __device__ __forceinline__ bool walk_start(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, uint32_t t,
+                                             uint32_t& s, uint64_t& npa, uint32_t& np) {
+    walk_begin(t);
+    if (ev == CEP_NONE) {
+      walk_fail(KE_NPE, t);
+      return false;
+    }
+    s = lookup(sk, first);
+    np = 0;
+    if (flags & kWalkEmit) {
+      out_put(t);
+      npa = out_put(0);
+      if (err) {
+        walk_fail(err, t);
+        return false;
+      }
+    }
+    return true;
+  }
+
+  __device__ __forceinline__ void walk_end(uint32_t flags, uint64_t npa, uint32_t np) {
+    if (flags & kWalkEmit) {
+      A.out[npa] = np;
       n_matches++;
       n_pairs += np;
     }
   }
 
+  __device__ __forceinline__ void walk_now(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v,
+                                           uint32_t t) {
+    uint32_t s = CEP_NONE, np = 0;
+    uint64_t npa = 0;
+    if (!walk_start(flags, sk, ev, first, t, s, npa, np)) return;
+    Dewey w = dw_pin(v);
+    while (walk_node(flags, s, w, t, 0, np)) {
+    }
+    if (!err) walk_end(flags, npa, np);
+  }
+
+  // Drains this lane's queue in order.  Called by every lane of the wave at once: the loop
+  // gives each lane one node per iteration, starting its next walk as soon as one ends.
+  __device__ __forceinline__ void flush() {
+    const uint32_t id0 = opc - wq_n;
+    uint32_t i = 0, s = CEP_NONE, t = 0, flags = 0, np = 0;
+    uint64_t npa = 0;
+    Dewey w;
+    dw_init(w, 0);
+    bool active = false;
+    for (;;) {
+      if (!active) {
+        if (i >= wq_n || err) break;
+        const v4u h = *WQ(i, 0);
+        flags = (h.x >> 8) & 0xFF;
+        w.n = h.x >> 24;
+        w.len = h.w;
+#pragma unroll
+        for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
+          v4u d = {0, 0, 0, 0};
+          if ((uint32_t)(2 * k) < w.n) d = *WQ(i, 1 + k);
+          w.v[2 * k] = (int32_t)d.x;
+          w.c[2 * k] = d.y;
+          if (2 * k + 1 < kDeweyPairs) {
+            w.v[2 * k + 1] = (int32_t)d.z;
+            w.c[2 * k + 1] = d.w;
+          }
+        }
+        w = dw_pin(w);
+        t = reinterpret_cast<const uint32_t*>(WQ(i, kWalkQuads - 1))[0];
+        i++;
+        if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
+        active = true;
+      }
+      if (!walk_node(flags, s, w, t, id0 + i - 1, np)) {
+        if (err) break;
+        walk_end(flags, npa, np);
+        active = false;
+      }
+    }
+    wq_n = 0;
+  }
+
   // ---------------------------------------------------------------- one event
   __device__ __forceinline__ void event(bool begin_hit) {
+    const uint32_t pf = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
-    pending = 0;
     n_final = 0;
     ocount = 0;
+    // prefetch the next event's fields (consumed by the next event() call)
+    EvT nev = ev;
+    const bool more = j + 1 < n_ev;
+    if (more) q.load_ev(nev, base + j + 1);
     const uint32_t n = count;
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
-      load(half, i, c);
+      load(half, i, c, pf);
       const int produced = q.step(*this, c);
       if (err) return;
       if (produced == 0) {  // removePattern
@@ -407,28 +608,20 @@ struct Lane {
     const uint32_t oh = half ^ 1u;
     half = oh;
     count = ocount;
-    // records created at this event learn the node chain of the event
-    if (pending) {
-      for (uint32_t i = 0; i < count; i++) {
-        v4u* hp = QP(oh, i, 0);
-        if ((*hp).z == kPending) (*hp).z = cur_first;
-      }
+    if (more) {
+      ev = nev;
+      ev_pos = j + 1;
     }
     if (!n_final) return;
     // matchConstruction: finals in order, then drop them from the queue
-    const uint32_t m0 = n_matches, p0 = n_pairs;
     uint32_t w = 0;
     for (uint32_t i = 0; i < count; i++) {
       const v4u hd = *QP(oh, i, 0);
       if (hd.x & kRecFinal) {
         Rec<F> r;
-        load(oh, i, r);
+        load(oh, i, r, cur_first);
         walk_remove(q.stage_sk(r.stage), r.event, r.ev_first, r.ver, true);
-        if (err) {  // nothing of this event is forwarded
-          n_matches = m0;
-          n_pairs = p0;
-          return;
-        }
+        if (err) return;
       } else {
         if (w != i) copy_rec(oh, i, w);
         w++;
@@ -441,39 +634,60 @@ struct Lane {
   // Lanes of a wavefront advance in lockstep; a lane whose queue holds only the begin run
   // (whose single BEGIN edge did not match) is in the reference's quiet state: an event
   // that fails the begin predicate changes nothing (the begin run is re-added with the same
-  // version, NFA.java:149-157), so the lane tests up to kQuietChunk events per step.
+  // version, NFA.java:149-157), so the lane tests kQuietChunk events per step with their
+  // loads issued together.
   __device__ __forceinline__ bool only_begin() const {
     if (kBeginReg) return count == 0;
     if (count != 1) return false;
     return ((*QP(half, 0, 0)).x & 0x00FFFFFFu) == q.begin_stage;
   }
 
-  __device__ __forceinline__ void run(uint32_t n, uint32_t* err_seq) {
+  __device__ __forceinline__ void run() {
+    const uint32_t n = n_ev;
     uint32_t jj = 0;
+    int pa_err = KE_OK;  // an exception of the per-event step (walks queued before it go first)
+    uint32_t pa_seq = 0;
     while (jj < n) {
-      bool hit = false, known = false;
-      (void)hit;
+      if (A.defer && __any(wq_n >= kWalkFlush)) {
+        flush();
+        if (err) break;
+      }
+      bool known = false;
       if (q.quiet && only_begin()) {
         const uint32_t lim = (n - jj > kQuietChunk) ? jj + kQuietChunk : n;
-        for (; jj < lim; jj++) {
-          j = jj;
-          hit = q.begin_pred(*this);
-          if (err || hit) break;
-        }
+        const uint32_t h = q.begin_scan(*this, jj, lim);
         if (err) {
-          *err_seq = jj;
-          return;
+          pa_err = err;
+          pa_seq = h;
+          break;
         }
-        if (!hit) continue;
-        known = true;
+        if (h >= lim) {
+          jj = lim;
+          continue;
+        }
+        jj = h;
+        known = true;  // the scan already found the begin predicate true
       }
       j = jj;
-      event(known);  // known: the quiet scan already found the begin predicate true
+      if (ev_pos != jj) {
+        q.load_ev(ev, base + jj);
+        ev_pos = jj;
+      }
+      event(known);
       if (err) {
-        *err_seq = jj;
-        return;
+        pa_err = err;
+        pa_seq = jj;
+        break;
       }
       jj++;
+    }
+    if (pa_err != KE_OK || !err) {
+      err = KE_OK;
+      flush();  // every lane of the wave together
+      if (!err && pa_err != KE_OK) {
+        err = pa_err;
+        err_seq = pa_seq;
+      }
     }
   }
 };
@@ -488,9 +702,10 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
   Lane<F, Q> L(A, q);
   L.key = key;
   L.base = A.key_off[key];
-  const uint32_t n = (uint32_t)(A.key_off[key + 1] - L.base);
+  L.n_ev = (uint32_t)(A.key_off[key + 1] - L.base);
   L.rb = reinterpret_cast<v4u*>(A.rings) +
-         (slot / 64) * (2ull * A.rcap * RecLayout<F>::kQuads * 64) + (slot % 64);
+         (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (slot % 64);
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
   // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
   L.bdig = 1;
   L.half = 0;
@@ -504,15 +719,14 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
     L.half = 0;
     L.count = 1;
   }
-  uint32_t err_seq = 0;
-  L.run(n, &err_seq);
+  L.run();
   KeyState& ks = A.ks[key];
   ks.n_matches = L.n_matches;
   ks.n_pairs = L.n_pairs;
   ks.out_first = L.out_first;
   ks.err = L.err;
-  ks.err_seq = err_seq;
-  if (L.err == KE_CAPACITY) atomicAdd(A.n_capacity_err, 1u);
+  ks.err_seq = L.err_seq;
+  if (L.err == KE_CAPACITY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
 }
 
 }  // namespace cep

@@ -120,7 +120,7 @@ struct cep_session {
   Cols cols{};
   int64_t watermark = INT64_MIN;
   // scratch
-  DBuf rings, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask;
+  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask;
 };
 
 namespace {
@@ -246,6 +246,8 @@ void run_nfa(cep_session* s, QueryRt& r) {
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   s->rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
+  const uint32_t wcap = 32;  // deferred walks per key between drains (nfa_lane.h)
+  s->walks.ensure(walkq_size(std::max<uint64_t>(nk, 1), wcap));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
@@ -257,6 +259,9 @@ void run_nfa(cep_session* s, QueryRt& r) {
   a.ts = s->ts;
   a.rings = s->rings.p;
   a.rcap = rcap;
+  a.walks = s->walks.p;
+  a.wcap = wcap;
+  a.defer = 1;
   a.key_list = nullptr;
   a.n_list = 0;
   a.nodes = s->nodes.as<Node>();
@@ -281,14 +286,15 @@ void run_nfa(cep_session* s, QueryRt& r) {
   HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   total_ms += ms;
 
-  // retry keys that hit a capacity limit with 8x the live-run ring and grown pools
+  // retry keys that hit a capacity limit with 8x the live-run ring and grown pools, and
+  // keys whose deferred walks conflicted (KE_CONFLICT), with walks in place
   for (int round = 0; h.n_cap_err > 0 && round < 3; round++) {
     std::vector<KeyState> hks(nk);
     HIPCHECK(hipMemcpyAsync(hks.data(), r.ks.p, sizeof(KeyState) * nk, hipMemcpyDeviceToHost, s->stream));
     HIPCHECK(hipStreamSynchronize(s->stream));
     std::vector<uint32_t> list;
     for (uint64_t k = 0; k < nk; k++)
-      if (hks[k].err == KE_CAPACITY) list.push_back((uint32_t)k);
+      if (hks[k].err == KE_CAPACITY || hks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
     if (list.empty()) break;
     rcap *= 8;
     s->keylist.ensure(sizeof(uint32_t) * list.size());
@@ -323,6 +329,7 @@ void run_nfa(cep_session* s, QueryRt& r) {
     a.out_pool.cap = (uint32_t)out_cap;
     a.rings = retry_rings.p;
     a.rcap = rcap;
+    a.defer = 0;
     a.key_list = s->keylist.as<uint32_t>();
     a.n_list = (uint32_t)list.size();
     HIPCHECK(hipEventRecord(s->ev0, s->stream));

@@ -1,0 +1,100 @@
+"""CPU build of a query's generated NFA kernel (test infrastructure, no GPU).
+
+The JIT source libcep generates for a query (compile.cpp generate_jit, on csrc/nfa_lane.h)
+is compiled as host C++ against tests/lane_cpu/hip/hip_runtime.h (stubs: one lane per
+wave, sequential atomics) and driven by tests/lane_cpu/driver.cpp, which mirrors
+session.cpp's run_nfa (pools, deferred-walk queues, retries with walks in place).  It runs
+the exact lane code the GPU runs, key by key, so the per-event logic and the deferred-walk
+machinery are checked against the oracle by `-m "not gpu"` tests; the GPU tests remain the
+parity tests proper.
+"""
+import ctypes as C
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+
+from kafkastreams_cep_amd import native as N
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "kafkastreams-cep_amd", "csrc")
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+BUILD = os.path.join(os.environ.get("TMPDIR", "/tmp"), "cep_lane_cpu")
+_libs = {}
+
+
+def build(ir: bytes):
+    """Compile the query's kernel for the host; returns the loaded library (cached)."""
+    src = N.Query(ir).jit_source
+    deps = "".join(open(os.path.join(CSRC, h)).read() for h in
+                   ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
+    deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
+    deps += open(os.path.join(HERE, "lane_cpu", "hip", "hip_runtime.h")).read()
+    key = hashlib.sha1((src + deps).encode()).hexdigest()[:16]
+    if key in _libs:
+        return _libs[key]
+    os.makedirs(BUILD, exist_ok=True)
+    qsrc = os.path.join(BUILD, f"q_{key}.hip")
+    so = os.path.join(BUILD, f"lane_{key}.so")
+    if not os.path.exists(so):
+        with open(qsrc, "w") as f:
+            f.write(src)
+        tmp = so + f".{os.getpid()}"
+        subprocess.check_call([CLANG, "-x", "c++", "-std=c++17", "-O1", "-g", "-rdynamic", "-shared", "-fPIC",
+                               "-ffp-contract=off", "-Wno-unused-value", "-w",
+                               f"-I{os.path.join(HERE, 'lane_cpu')}", f"-I{CSRC}",
+                               f'-DQUERY_SRC="{qsrc}"', os.path.join(HERE, "lane_cpu", "driver.cpp"),
+                               "-o", tmp])
+        os.replace(tmp, so)
+    lib = C.CDLL(so)
+    lib.lane_run.argtypes = [C.c_uint64, C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_void_p,
+                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]
+    lib.lane_n_matches.restype = C.c_uint64
+    lib.lane_n_pairs.restype = C.c_uint64
+    lib.lane_fetch.argtypes = [C.c_void_p] * 7
+    _libs[key] = lib
+    return lib
+
+
+def run(ir, key_off, cols, rcap=32, defer=True):
+    """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest)."""
+    lib = build(ir)
+    key_off = np.ascontiguousarray(key_off, np.uint64)
+    cols = [np.ascontiguousarray(c) for c in cols]
+    ptrs = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+    nk = len(key_off) - 1
+    retried = C.c_uint32()
+    lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried))
+    nm, npairs = lib.lane_n_matches(), lib.lane_n_pairs()
+    key = np.zeros(nm, np.uint32)
+    emit = np.zeros(nm, np.uint32)
+    off = np.zeros(nm + 1, np.uint64)
+    seq = np.zeros(npairs, np.uint32)
+    stage = np.zeros(npairs, np.uint16)
+    err = np.zeros(nk, np.int32)
+    err_seq = np.zeros(nk, np.uint32)
+    lib.lane_fetch(*[a.ctypes.data for a in (key, emit, off, seq, stage, err, err_seq)])
+    m = {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
+         "pair_seq": seq, "pair_stage": stage, "err_code": err, "err_seq": err_seq,
+         "retried": retried.value}
+    m["emit_pos"] = (key_off[key.astype(np.int64)] + emit).astype(np.uint64)
+    pk = np.repeat(key.astype(np.int64), np.diff(off.astype(np.int64)))
+    m["pair_pos"] = (key_off[pk] + seq).astype(np.uint64)
+    return m
+
+
+def assert_same(g, r, key_off):
+    """lane result `g` equals oracle result `r` exactly (as gpu_helpers.assert_parity, no digest)."""
+    assert g["n_matches"] == r["n_matches"], (g["n_matches"], r["n_matches"])
+    assert g["n_pairs"] == r["n_pairs"]
+    np.testing.assert_array_equal(g["key"], r["key"])
+    np.testing.assert_array_equal(g["emit_pos"], r["emit_pos"].astype(np.uint64))
+    np.testing.assert_array_equal(g["pair_off"], r["pair_off"])
+    np.testing.assert_array_equal(g["pair_pos"], r["pair_pos"].astype(np.uint64))
+    np.testing.assert_array_equal(g["pair_stage"], r["pair_stage"])
+    np.testing.assert_array_equal(g["err_code"], r["err_code"])
+    off = np.asarray(key_off, np.uint64)
+    bad = r["err_code"] != 0
+    np.testing.assert_array_equal(g["err_seq"][bad].astype(np.uint64) + off[:-1][bad],
+                                  r["err_pos"][bad].astype(np.uint64))

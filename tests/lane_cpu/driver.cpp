@@ -1,0 +1,133 @@
+// CPU driver of a generated NFA kernel (test infrastructure): the host side of
+// session.cpp run_nfa - pools, deferred-walk queues, capacity/conflict retries with walks in
+// place - with the kernel run lane by lane, then the matches flattened in key order.
+// Built per query by tests/lane_cpu.py with QUERY_SRC = the query's generated source.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdint>
+#include <vector>
+
+#include QUERY_SRC
+
+thread_local LaneDim3 blockIdx, threadIdx, blockDim;
+
+namespace {
+std::vector<uint32_t> g_key, g_emit, g_seq;
+std::vector<uint64_t> g_off;
+std::vector<uint16_t> g_stage;
+std::vector<int32_t> g_err;
+std::vector<uint32_t> g_err_seq;
+}  // namespace
+
+static void on_fault(int sig) {  // a lane bug: print where, then die
+  void* bt[32];
+  const int n = backtrace(bt, 32);
+  backtrace_symbols_fd(bt, n, 2);
+  _exit(128 + sig);
+}
+
+extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const* cols, int n_cols,
+                        const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried) {
+  using namespace cep;
+  signal(SIGSEGV, on_fault);
+  const uint64_t ne = key_off[nk];
+  std::vector<Node> nodes(ne * 4 + nk * 64 + 4096);
+  std::vector<Pred> preds(ne * 4 + nk * 64 + 4096);
+  std::vector<uint32_t> out((ne + nk * 4 + 64) * 2 * kOutChunkWords);
+  std::vector<KeyState> ks(nk);
+  // device pools are not cleared between batches: start from garbage, not zeros
+  auto scribble = [](void* p, size_t n) {
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (size_t i = 0; i + 8 <= n; i += 8) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      std::memcpy((char*)p + i, &x, 8);
+    }
+  };
+  scribble(nodes.data(), nodes.size() * sizeof(Node));
+  scribble(preds.data(), preds.size() * sizeof(Pred));
+  scribble(out.data(), out.size() * 4);
+  uint32_t node_top = 0, pred_top = 0, out_top = 0, n_cap = 0;
+  NfaArgs a{};
+  a.n_keys = nk;
+  a.key_off = key_off;
+  for (int f = 0; f < n_cols; f++) a.cols.p[f] = cols[f];
+  a.ts = ts;
+  a.nodes = nodes.data();
+  a.preds = preds.data();
+  a.out = out.data();
+  a.node_pool = Pool{&node_top, (uint32_t)nodes.size(), 16};
+  a.pred_pool = Pool{&pred_top, (uint32_t)preds.size(), 16};
+  a.out_pool = Pool{&out_top, (uint32_t)(out.size() / kOutChunkWords), 1};
+  a.ks = ks.data();
+  a.n_capacity_err = &n_cap;
+  auto launch = [&](uint64_t nslots, uint32_t rc, int df) {
+    std::vector<v4u> rings(ring_bytes(8, nslots, rc) / 16 + 64);
+    std::vector<v4u> walks(walkq_bytes(nslots, 32) / 16 + 64);
+    scribble(rings.data(), rings.size() * 16);
+    scribble(walks.data(), walks.size() * 16);
+    a.rings = rings.data();
+    a.rcap = rc;
+    a.walks = walks.data();
+    a.wcap = 32;
+    a.defer = (uint32_t)df;
+    blockDim.x = 256;
+    for (uint64_t s = 0; s < nslots; s++) {
+      blockIdx.x = (unsigned)(s / 256);
+      threadIdx.x = (unsigned)(s % 256);
+      cep_nfa_jit(a);
+    }
+  };
+  launch(nk, rcap, defer);
+  *n_retried = 0;
+  for (int round = 0; n_cap > 0 && round < 3; round++) {  // session.cpp run_nfa
+    std::vector<uint32_t> list;
+    for (uint64_t k = 0; k < nk; k++)
+      if (ks[k].err == KE_CAPACITY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
+    *n_retried += (uint32_t)list.size();
+    n_cap = 0;
+    rcap *= 8;
+    a.key_list = list.data();
+    a.n_list = (uint32_t)list.size();
+    launch(list.size(), rcap, 0);
+  }
+  g_key.clear(); g_emit.clear(); g_seq.clear(); g_off.assign(1, 0); g_stage.clear();
+  g_err.resize(nk); g_err_seq.resize(nk);
+  for (uint64_t k = 0; k < nk; k++) {
+    g_err[k] = ks[k].err;
+    g_err_seq[k] = ks[k].err_seq;
+    uint32_t chunk = ks[k].out_first, pos = 0;
+    auto next = [&]() -> uint32_t {
+      if (pos == kOutChunkWords - 1) {
+        chunk = out[(uint64_t)chunk * kOutChunkWords + kOutChunkWords - 1];
+        pos = 0;
+      }
+      return out[(uint64_t)chunk * kOutChunkWords + pos++];
+    };
+    for (uint32_t m = 0; m < ks[k].n_matches; m++) {
+      g_key.push_back((uint32_t)k);
+      g_emit.push_back(next());
+      const uint32_t np = next();
+      for (uint32_t i = 0; i < np; i++) {
+        g_seq.push_back(next());
+        g_stage.push_back((uint16_t)next());
+      }
+      g_off.push_back(g_seq.size());
+    }
+  }
+  return 0;
+}
+
+extern "C" uint64_t lane_n_matches() { return g_key.size(); }
+extern "C" uint64_t lane_n_pairs() { return g_seq.size(); }
+extern "C" void lane_fetch(uint32_t* key, uint32_t* emit, uint64_t* off, uint32_t* seq, uint16_t* stage,
+                           int32_t* err, uint32_t* err_seq) {
+  std::memcpy(key, g_key.data(), 4 * g_key.size());
+  std::memcpy(emit, g_emit.data(), 4 * g_emit.size());
+  std::memcpy(off, g_off.data(), 8 * g_off.size());
+  std::memcpy(seq, g_seq.data(), 4 * g_seq.size());
+  std::memcpy(stage, g_stage.data(), 2 * g_stage.size());
+  std::memcpy(err, g_err.data(), 4 * g_err.size());
+  std::memcpy(err_seq, g_err_seq.data(), 4 * g_err_seq.size());
+}

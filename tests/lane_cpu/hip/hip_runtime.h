@@ -1,0 +1,40 @@
+// CPU stand-in for the HIP device runtime: lets tests/lane_cpu build a query's generated NFA
+// kernel (compile.cpp generate_jit + csrc/nfa_lane.h) as ordinary host code, one lane at a
+// time, to debug and fuzz the lane logic without a GPU.  Test infrastructure only.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#define __device__
+#define __host__
+#define __global__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define asm(...) ((void)0)
+
+struct LaneDim3 {
+  unsigned x = 0, y = 0, z = 0;
+};
+extern thread_local LaneDim3 blockIdx, threadIdx, blockDim;
+
+inline unsigned atomicAdd(unsigned* p, unsigned v) {
+  const unsigned o = *p;
+  *p += v;
+  return o;
+}
+inline bool __any(int x) { return x != 0; }  // a wave of one lane
+inline double __longlong_as_double(long long x) {
+  double d;
+  std::memcpy(&d, &x, 8);
+  return d;
+}
+inline long long __double_as_longlong(double d) {
+  long long x;
+  std::memcpy(&x, &d, 8);
+  return x;
+}
+inline double __dadd_rn(double a, double b) { return a + b; }
+inline double __dsub_rn(double a, double b) { return a - b; }
+inline double __dmul_rn(double a, double b) { return a * b; }
+inline double __ddiv_rn(double a, double b) { return a / b; }
