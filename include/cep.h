@@ -183,7 +183,7 @@ int cep_watermark(cep_session* s, int64_t* out);
 
 /* Device time of the last batch, per query, from HIP events recorded on the session
  * stream (ms): the matching kernel launches (kernel_ms, `launches` of them: the NFA kernel
- * incl. capacity retries, or stencil_mask + stencil_scan + stencil_emit) and the
+ * incl. capacity retries, or stencil_mask + stencil_emit) and the
  * setup/compaction kernels (aux_ms). */
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);
 

@@ -150,10 +150,10 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint64_t n_tiles = stencil_tiles(s->n_events);
   const uint64_t nb = (nk + 1023) / 1024;
   s->tile_key.ensure(sizeof(uint32_t) * 2 * (n_tiles + 1));                    // tile rank + count
-  s->status.ensure(sizeof(uint64_t) * (n_tiles + 1));                           // tile offsets
-  s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));
+  s->status.ensure(sizeof(uint32_t) * (n_tiles / 64 + 2));                       // group counts
+  s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
   s->keylist.ensure(sizeof(uint32_t) * (2 * nk + nb + 2));                       // rank, nz_key, bsum
-  s->bnd.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));
+  s->bnd.ensure(sizeof(uint64_t) * (s->n_events / 64 + 8));
   s->scratch.ensure(sizeof(Scratch));
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
@@ -188,14 +188,15 @@ void run_stencil(cep_session* s, QueryRt& r) {
   for (uint32_t x = 0; x < m && x < 8; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
   a.tile_cnt = s->tile_key.as<uint32_t>() + (n_tiles + 1);
-  a.tile_off = s->status.as<uint64_t>();
+  a.group_cnt = s->status.as<uint32_t>();
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
   a.total = &sc->total;
   a.out_cap = cap;
   a.overflow = &sc->overflow;
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
-  HIPCHECK(hipMemsetAsync(s->bnd.p, 0, sizeof(uint64_t) * (s->n_events / 64 + 2), s->stream));
+  HIPCHECK(hipMemsetAsync(s->bnd.p, 0, sizeof(uint64_t) * (s->n_events / 64 + 8), s->stream));
+  HIPCHECK(hipMemsetAsync(s->status.p, 0, sizeof(uint32_t) * (n_tiles / 64 + 2), s->stream));
   HIPCHECK(launch_key_index(s->key_off, nk, s->n_events, rank, bsum, nz_key, s->bnd.as<uint64_t>(),
                             s->tile_key.as<uint32_t>(), s->stream));
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
@@ -206,7 +207,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   HIPCHECK(hipStreamSynchronize(s->stream));
   HIPCHECK(hipEventElapsedTime(&r.kernel_ms, s->ev0, s->ev1));
   HIPCHECK(hipEventElapsedTime(&r.aux_ms, s->ev2, s->ev0));
-  r.launches = 3;  // stencil_mask + stencil_scan + stencil_emit
+  r.launches = 2;  // stencil_mask + stencil_emit
   if (h.overflow) throw std::runtime_error("stencil output overflow");
   r.n_matches = h.total;
   r.n_pairs = h.total * m;

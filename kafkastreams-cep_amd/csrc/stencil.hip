@@ -14,12 +14,12 @@
 // from a bitmap built once per batch, so a window crossing a key start is masked with
 // shifts, and a match's key is the tile's first key advanced by the key starts before it.
 //
-// Passes.  (1) stencil_mask streams the column once and writes one 64-bit match mask per 64
-// events (1 bit/event) and a count per tile; (2) a single-block scan turns tile counts into
-// output offsets; (3) stencil_emit reads the masks back (1/32 of the column's bytes) and
-// writes the matches in order.  Nothing waits on another workgroup, so the streaming pass
-// runs at HBM rate (a single-pass decoupled look-back was measured latency-bound here:
-// rounds of co-resident tiles look back through each other, profiles/README.md).
+// Passes.  (1) stencil_mask streams the column once (a wave issues all its loads before the
+// first is used) and writes one 64-bit match mask per 64 events (1 bit/event) and a count per
+// tile; (2) stencil_emit sums the counts of the tiles before its own, reads the masks back
+// (1/32 of the column's bytes) and writes the matches in order.  No tile waits on another, so the streaming pass runs at HBM rate (a single-pass
+// decoupled look-back was measured latency-bound here: rounds of co-resident tiles look back
+// through each other).
 #include <hip/hip_runtime.h>
 
 #include "cep_layout.h"
@@ -33,6 +33,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kStThreads = 256;
 constexpr int kStPer = 64;  // events per thread (one 64-bit mask)
 constexpr uint64_t kStTile = (uint64_t)kStThreads * kStPer;
+constexpr uint64_t kStGroup = 64;  // tiles per group count (stencil_emit's offsets)
 
 // ---------------------------------------------------------------- per-batch key index
 // rank[k] = number of non-empty keys before k (two-level exclusive scan)
@@ -140,6 +141,13 @@ struct StEval {
       P[s] |= (ok ? 1u : 0u) << bit;
     }
   }
+  // stage s over one event per lane, straight into a ballot word: each compare's own lane
+  // mask (llvm.amdgcn.ballot of a compare is the v_cmp result), ANDed in scalar registers
+  __device__ __forceinline__ uint64_t ballot(int s, int32_t x0, int32_t x1) const {
+    uint64_t m = __builtin_amdgcn_ballot_w64(x0 >= lo[s][0]) & __builtin_amdgcn_ballot_w64(x0 <= hi[s][0]);
+    if (NCOL > 1) m &= __builtin_amdgcn_ballot_w64(x1 >= lo[s][1]) & __builtin_amdgcn_ballot_w64(x1 <= hi[s][1]);
+    return m;
+  }
   __device__ __forceinline__ void one(const StencilArgs& A, uint64_t p, uint32_t* P, int bit) const {
     if (p >= A.n_events) return;
     if (RANGE) {
@@ -157,14 +165,24 @@ struct StEval {
 
 template <int M, bool RANGE, int NCOL>
 __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
-  constexpr int H = M - 1;  // events a window reaches back
+  constexpr int H = M - 1;              // events a window reaches back
+  constexpr int D = NCOL > 1 ? 8 : 16;  // steps whose loads are issued together
   __shared__ uint32_t s_cnt[kStThreads / 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
+  // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
   const StEval<M, RANGE, NCOL> ev(A);
-  // carries: nibbles of the 8 events before the step (c1: -4..-1, c2: -8..-5), wave-uniform
-  uint32_t c1[M], c2[M];
-  uint32_t bc1 = 0, bc2 = 0;
+  // the wave's 64 key-start words, one per lane (word w: events 64 w .. 64 w + 63)
+  uint64_t bw = 0;
+  if (H > 0 && wbase + (uint64_t)lane * 64 < A.n_events) bw = A.bnd[wbase / 64 + lane];
+  const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events;
+  // steps with a key start (bit 4q + x: word x of step q is non-zero), mostly none
+  const uint64_t kstep = H > 0 ? __ballot(bw != 0) : 0;
+  // Ballot words of the previous step: bit l of W[s][k] = stage s holds at event 4l + k.
+  // Only their top two bits are read (events 4*62+k, 4*63+k): seed them with the 8 events
+  // before the wave.
+  uint64_t pW[M][4], pK[4];
   {
     uint32_t P[M];
 #pragma unroll
@@ -172,118 +190,151 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
     if (H > 0 && lane < 8 && wbase >= (uint64_t)(8 - lane)) ev.one(A, wbase - 8 + lane, P, 0);
 #pragma unroll
     for (int s = 0; s < M; s++) {
-      const uint64_t b = __ballot(P[s] & 1u);
-      c2[s] = (uint32_t)b & 0xF;
-      c1[s] = (uint32_t)(b >> 4) & 0xF;
+      const uint64_t b = __ballot(P[s] & 1u);  // bit x: event wbase - 8 + x
+#pragma unroll
+      for (int k = 0; k < 4; k++) pW[s][k] = (((b >> k) & 1ull) << 62) | (((b >> (4 + k)) & 1ull) << 63);
     }
-    if (H > 0 && wbase >= 8) {  // key-start bits of events wbase-8 .. wbase-1 (wbase % 64 == 0)
-      const uint64_t w = A.bnd[wbase / 64 - 1];
-      bc2 = (uint32_t)(w >> 56) & 0xF;
-      bc1 = (uint32_t)(w >> 60) & 0xF;
-    }
+    const uint64_t w = (H > 0 && wbase >= 8) ? A.bnd[wbase / 64 - 1] : 0;  // wbase % 64 == 0
+#pragma unroll
+    for (int k = 0; k < 4; k++) pK[k] = (((w >> (56 + k)) & 1ull) << 62) | (((w >> (60 + k)) & 1ull) << 63);
   }
   uint32_t cnt = 0;
-#pragma unroll 4
-  for (int q = 0; q < kStSteps; q++) {
-    const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
-    uint32_t P[M];
-#pragma unroll
-    for (int s = 0; s < M; s++) P[s] = 0;
-    if (RANGE && A.aligned && e0 + 4 <= A.n_events) {
-      const v4i x = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0));
-      v4i y = x;
-      if (NCOL > 1) y = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0));
-      ev.range(x.x, y.x, P, 0);
-      ev.range(x.y, y.y, P, 1);
-      ev.range(x.z, y.z, P, 2);
-      ev.range(x.w, y.w, P, 3);
-    } else if (e0 < A.n_events) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) ev.one(A, e0 + i, P, i);
-    }
-    uint32_t B = 0;
-    if (H > 0 && e0 < A.n_events) B = (uint32_t)(A.bnd[e0 / 64] >> (e0 % 64)) & 0xF;
-    // 12-bit windows: [11:8] this nibble, [7:4] the 4 events before, [3:0] the 4 before that
-    uint32_t match = 0xF;
-#pragma unroll
-    for (int s = 0; s < M; s++) {
-      uint32_t w = P[s] << 8;
-      if (H > 0) {
-        const uint32_t u1 = __shfl_up(P[s], 1, 64), u2 = __shfl_up(P[s], 2, 64);
-        const uint32_t p1 = lane >= 1 ? u1 : c1[s];
-        const uint32_t p2 = lane >= 2 ? u2 : (lane == 1 ? c1[s] : c2[s]);
-        w |= (p1 << 4) | p2;
-        c2[s] = __shfl(P[s], 62, 64);
-        c1[s] = __shfl(P[s], 63, 64);
-      }
-      // stage s sits at offset -(M-1-s) from the window's last event
-      match &= w >> (8 - (M - 1 - s));
-    }
-    if (H > 0) {
-      const uint32_t u1 = __shfl_up(B, 1, 64), u2 = __shfl_up(B, 2, 64);
-      const uint32_t b1 = lane >= 1 ? u1 : bc1;
-      const uint32_t b2 = lane >= 2 ? u2 : (lane == 1 ? bc1 : bc2);
-      const uint32_t bw = (B << 8) | (b1 << 4) | b2;
-      // a key start at any of the window's last M-1 events (not its first) kills it
-      uint32_t sm = 0;
-#pragma unroll
-      for (int x = 0; x < H; x++) sm |= bw << x;
-      match &= ~(sm >> 8);
-      bc2 = __shfl(B, 62, 64);
-      bc1 = __shfl(B, 63, 64);
-    }
-    match &= 0xF;
-    if (e0 + 4 > A.n_events) match &= e0 >= A.n_events ? 0u : ((1u << (A.n_events - e0)) - 1);
-    cnt += __popc(match);
-    // 16 lanes -> one 64-bit mask word
-    uint64_t word = (uint64_t)match << (4 * (lane & 15));
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) word |= __shfl_xor(word, o, 64);
-    if ((lane & 15) == 0 && e0 < A.n_events) A.mask[e0 / 64] = word;
+  uint64_t myword = 0;  // mask word wbase / 64 + lane = word k of step q for lane 4q + k
+  // one step per iteration, the next step's load in flight (occupancy supplies the rest of
+  // the memory parallelism; the step body is scalar-heavy and must not be unrolled 16x)
+  v4i xn = {0, 0, 0, 0}, yn = {0, 0, 0, 0};
+  if (fast) {
+    xn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + wbase + (uint64_t)lane * 4));
+    if (NCOL > 1) yn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + wbase + (uint64_t)lane * 4));
   }
+#pragma unroll 1
+  for (int q = 0; q < kStSteps; q++) {
+    {
+      const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
+      const v4i x = xn, y = NCOL > 1 ? yn : xn;
+      if (fast && q + 1 < kStSteps) {
+        xn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0 + 256));
+        if (NCOL > 1) yn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0 + 256));
+      }
+      // stage words of this step (wave-uniform, scalar registers): bit l of W[s][k] = stage s
+      // holds at event 4l + k
+      uint64_t W[M][4];
+      if (fast) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
+        for (int s = 0; s < M; s++) {
+          W[s][0] = ev.ballot(s, x.x, y.x);
+          W[s][1] = ev.ballot(s, x.y, y.y);
+          W[s][2] = ev.ballot(s, x.z, y.z);
+          W[s][3] = ev.ballot(s, x.w, y.w);
+        }
+      } else {
+        uint32_t P[M];
+#pragma unroll
+        for (int s = 0; s < M; s++) P[s] = 0;
+        if (RANGE && A.aligned && e0 + 4 <= A.n_events) {
+          const v4i xs = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0));
+          v4i ys = xs;
+          if (NCOL > 1) ys = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0));
+          ev.range(xs.x, ys.x, P, 0);
+          ev.range(xs.y, ys.y, P, 1);
+          ev.range(xs.z, ys.z, P, 2);
+          ev.range(xs.w, ys.w, P, 3);
+        } else if (e0 < A.n_events) {  // events past the end stay 0: no window can end there
+#pragma unroll
+          for (int i = 0; i < 4; i++) ev.one(A, e0 + i, P, i);
+        }
+#pragma unroll
+        for (int s = 0; s < M; s++)
+#pragma unroll
+          for (int k = 0; k < 4; k++) W[s][k] = __builtin_amdgcn_ballot_w64((P[s] >> k) & 1u);
+      }
+      uint64_t K[4] = {0, 0, 0, 0};
+      if (H > 0 && ((kstep >> (4 * q)) & 0xF)) {
+        // this lane's 4 key-start bits: word 4q + lane/16 of the wave (lanes 4q..4q+3 hold
+        // them), nibble lane % 16
+        const uint64_t b0 = __shfl(bw, 4 * q, 64), b1 = __shfl(bw, 4 * q + 1, 64);
+        const uint64_t b2 = __shfl(bw, 4 * q + 2, 64), b3 = __shfl(bw, 4 * q + 3, 64);
+        const int g = lane >> 4;
+        const uint64_t bword = g == 0 ? b0 : g == 1 ? b1 : g == 2 ? b2 : b3;
+        const uint32_t B = (uint32_t)(bword >> (4 * (lane & 15))) & 0xF;
+#pragma unroll
+        for (int k = 0; k < 4; k++) K[k] = __builtin_amdgcn_ballot_w64((B >> k) & 1u);
+      }
+      // word k: windows ending at events 4l + k.  Stage s sits o = M-1-s events back: event
+      // 4l + k - o is word (k - o) mod 4, `cr` lanes back (bits shifted up, the previous
+      // step's top bits carried in).  A key start at any of the window's last M-1 events
+      // (offsets 0 .. M-2) kills it.
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int s = 0; s < M; s++) {
+          const int t = k - (M - 1 - s);
+          const int cr = t >= 0 ? 0 : (3 - t) / 4;
+          const int kk = t + 4 * cr;
+          m &= cr == 0 ? W[s][kk] : ((W[s][kk] << cr) | (pW[s][kk] >> (64 - cr)));
+        }
+#pragma unroll
+        for (int o = 0; o < H; o++) {
+          const int t = k - o;
+          const int cr = t >= 0 ? 0 : (3 - t) / 4;
+          const int kk = t + 4 * cr;
+          m &= ~(cr == 0 ? K[kk] : ((K[kk] << cr) | (pK[kk] >> (64 - cr))));
+        }
+        cnt += (uint32_t)__popcll(m);
+        if (lane == 4 * q + k) myword = m;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int s = 0; s < M; s++) pW[s][k] = W[s][k];
+        pK[k] = K[k];
+      }
+    }
+  }
+  // one 512-B store: words 4q..4q+3 belong to step q (written when the step has an event)
+  if (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) A.mask[wbase / 64 + lane] = myword;
   if (lane == 0) s_cnt[wv] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) A.tile_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  if (threadIdx.x == 0) {
+    const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    A.tile_cnt[blockIdx.x] = c;
+    if (c) atomicAdd(A.group_cnt + blockIdx.x / kStGroup, c);  // per 64 tiles, for stencil_emit
+  }
 }
 
-// exclusive scan of the tile counts (one block; ~n_tiles/1024 sequential per thread)
-__global__ void __launch_bounds__(1024) stencil_scan(const uint32_t* cnt, uint64_t n, uint64_t* off, uint64_t* total) {
-  __shared__ uint64_t s[1024];
-  const uint64_t per = (n + 1023) / 1024;
-  const uint64_t a = threadIdx.x * per, b = (a + per < n) ? a + per : n;
-  uint64_t sum = 0;
-  for (uint64_t i = a; i < b; i++) sum += cnt[i];
-  s[threadIdx.x] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint64_t y = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += y;
-    __syncthreads();
-  }
-  uint64_t acc = s[threadIdx.x] - sum;
-  for (uint64_t i = a; i < b; i++) {
-    off[i] = acc;
-    acc += cnt[i];
-  }
-  if (threadIdx.x == 1023) *total = s[1023];
+// bit m of a 16-bit value -> bit 4 m
+__device__ __forceinline__ uint64_t spread4(uint32_t x16) {
+  uint64_t x = x16;
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
 }
 
+// Pass 2: a thread per 64 events (a quarter of a step's ballot words), the tile's offset
+// from the group and tile counts, a block scan for the threads' offsets and key ranks.
 template <int M>
 __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   __shared__ uint32_t s_wsum[kStThreads / 64];
+  __shared__ uint64_t s_toff[kStThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t t = blockIdx.x;
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
-  uint64_t match = 0, B = 0;
+  // the step (256 events) holding this thread's 64: 16 lanes of each of its 4 ballot words
+  uint32_t ck[4] = {0, 0, 0, 0};
+  uint64_t B = 0;
   if (p0 < A.n_events) {
-    match = A.mask[p0 / 64];
+    const uint64_t* w = A.mask + (p0 / 256) * 4;
+    const int sh = 16 * (int)((p0 / 64) & 3);
+#pragma unroll
+    for (int k = 0; k < 4; k++) ck[k] = (uint32_t)(w[k] >> sh) & 0xFFFFu;
     B = A.bnd[p0 / 64];
   }
   const uint64_t Bk = (tid == 0) ? (B & ~1ull) : B;  // key starts after the tile's first event
-  const uint32_t cnt = (uint32_t)__popcll(match), bc = (uint32_t)__popcll(Bk);
+  const uint32_t cnt = __popc(ck[0]) + __popc(ck[1]) + __popc(ck[2]) + __popc(ck[3]);
+  const uint32_t bc = (uint32_t)__popcll(Bk);
   // block exclusive scan of (matches, key starts), packed 16|16 (each <= 16384 per tile)
   const uint32_t packed = (cnt << 16) | bc;
   uint32_t incl = packed;
@@ -292,17 +343,30 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
     const uint32_t y = __shfl_up(incl, o, 64);
     if (lane >= o) incl += y;
   }
+  // this tile's output offset: the groups of 64 tiles before its own, then the tiles of its
+  // group before it (cheaper than a scan launch between the passes)
+  uint64_t part = 0;
+  const uint64_t g0 = (t / kStGroup) * kStGroup;
+  for (uint64_t i = tid; i < t / kStGroup; i += kStThreads) part += A.group_cnt[i];
+  if (g0 + tid < t) part += A.tile_cnt[g0 + tid];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
   if (lane == 63) s_wsum[wv] = incl;
+  if (lane == 0) s_toff[wv] = part;
   __syncthreads();
   uint32_t woff = 0;
 #pragma unroll
   for (int w = 0; w < kStThreads / 64; w++)
     if (w < wv) woff += s_wsum[w];
   const uint32_t excl = woff + incl - packed;
-  uint64_t o = A.tile_off[t] + (excl >> 16);
+  const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
+  if (t + 1 == gridDim.x && tid == kStThreads - 1) *A.total = toff + ((woff + incl) >> 16);  // all matches
+  uint64_t o = toff + (excl >> 16);
   const uint32_t rank0 = A.tile_rank[t] + (excl & 0xFFFF);
   uint32_t cur_rank = 0xFFFFFFFFu, key = 0;
   uint64_t kstart = 0;
+  // natural order: event p0 + 4 l + k is bit l of ck[k] -> bit 4 l + k
+  uint64_t match = spread4(ck[0]) | (spread4(ck[1]) << 1) | (spread4(ck[2]) << 2) | (spread4(ck[3]) << 3);
   while (match) {
     const int i = __builtin_ctzll(match);
     match &= match - 1;
@@ -342,7 +406,6 @@ hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
   hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
-  hipLaunchKernelGGL(stencil_scan, dim3(1), dim3(1024), 0, st, a.tile_cnt, n_tiles, a.tile_off, a.total);
   hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }

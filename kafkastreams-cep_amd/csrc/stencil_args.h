@@ -26,13 +26,13 @@ struct StencilArgs {
   uint16_t stage_name[8];    // walk order: stage name of pair t (t = 0 is the final event)
   bool aligned;              // col[] 16-B aligned: vector loads
   // pass 1 -> pass 3
-  uint64_t* mask;            // bit i of word w: a match ends at event 64 w + i
-  uint32_t* tile_cnt;        // matches per tile (pass 1), exclusive offsets after the scan
-  uint64_t* tile_off;
+  uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k
+  uint32_t* tile_cnt;        // matches per tile (pass 1)
+  uint32_t* group_cnt;       // matches per 64 tiles (pass 1, atomics; zeroed per batch)
   // output
   uint32_t* m_key;
   uint32_t* p_seq;           // [n_matches * m]
-  uint64_t* total;           // number of matches (stencil_scan)
+  uint64_t* total;           // number of matches (written by the last tile of stencil_emit)
   uint64_t out_cap;          // matches that fit the output arrays
   uint32_t* overflow;
 };
