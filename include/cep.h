@@ -52,6 +52,9 @@ extern "C" {
 #define CEP_KEY_ARITHMETIC 3     /* ArithmeticException (integer / or % by zero in a lambda) */
 #define CEP_KEY_CAPACITY 16      /* this build only: a per-key limit (live runs, Dewey width,
                                     buffer pools) was exceeded; never silent */
+#define CEP_KEY_CONFLICT 17      /* internal: a deferred buffer walk would have changed what a
+                                    later step saw; such keys are re-run with walks in place and
+                                    the code never reaches the caller */
 
 /* ---- compile-time errors, returned in cep_query_info.compile_error ---- */
 #define CEP_COMPILE_NPE 1              /* pattern ending in a Kleene/optional stage (StatesFactory:102) */
@@ -118,6 +121,10 @@ typedef struct {
   int tier;               /* CEP_TIER_JIT (default) or CEP_TIER_INTERP */
   uint32_t max_runs;      /* live runs per key (0 = default 32); retried x8 on overflow */
   double pool_factor;     /* buffer pool size per event of the batch (0 = default) */
+  int streaming;          /* 1: a key's NFA state carries over from one batch to the next (its
+                             events in consecutive batches are one stream, sequence numbers
+                             continue; every batch has the same n_keys); 0: every batch starts
+                             every key from the initial state */
 } cep_opts;
 
 int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts,
@@ -140,9 +147,14 @@ typedef struct {
   int memory;               /* CEP_MEM_HOST or CEP_MEM_DEVICE */
 } cep_batch;
 
-/* Runs every query of the session over the batch.  Each batch starts every key from the
- * NFA's initial state (one batch = one stream segment per key).  Returns once the batch's
- * kernels have completed (buffers are borrowed for the call only). */
+/* Runs every query of the session over the batch: a run of process() calls per key.  In a
+ * streaming session (cep_opts.streaming) the batch continues each key's stream where the
+ * previous batch left it (run queue, shared buffer, folds, sequence numbers); otherwise every
+ * batch starts every key from the NFA's initial state.  A streaming session cannot re-run a
+ * key: one that hits a limit (CEP_KEY_CAPACITY: size max_runs for the query) stops there,
+ * like a key whose query threw; its buffer walks run in place (no CEP_KEY_CONFLICT), and
+ * stencil-kind queries run on the NFA kernel.  Returns once the batch's kernels have
+ * completed (buffers are borrowed for the call only). */
 int cep_push_batch(cep_session* s, const cep_batch* b);
 int cep_sync(cep_session* s);
 

@@ -105,6 +105,22 @@ struct alignas(16) Pred {
   uint32_t pair[2 * kDeweyPairs];  // v0, c0, v1, c1, ...
 };
 
+// ---- per-key NFA state carried from one batch to the next (streaming sessions): what the
+// reference keeps in its NFA between process() calls (nfa/NFA.java:50-56) besides the run
+// records (the ring) and the buffer (the pools)
+struct KeyCarry {
+  uint32_t live;       // 1 once the key's NFA exists (initComputationStates done)
+  uint32_t seq;        // events consumed so far = sequence number of the next event
+  uint32_t half, count;
+  uint32_t bdig;       // begin run's version digit (kBeginReg)
+  uint32_t cur_first;  // node chain of the last event (resolves its records' kPending)
+  uint32_t ncur, nend, pcur, pend;  // pool chunks in hand
+  uint32_t opc;        // walks queued so far (deferred-walk ids)
+  int32_t err;         // sticky: the exception that stopped the key
+  uint32_t err_seq;
+  uint32_t pad[3];
+};
+
 // ---- per-key state kept between kernel phases
 struct KeyState {
   uint32_t n_matches;

@@ -36,6 +36,7 @@ struct NfaArgs {
   uint32_t* out;             // output chunks (kOutChunkWords words each)
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;
+  KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
   uint32_t* n_capacity_err;  // keys that hit CEP_KEY_CAPACITY
 };
 

@@ -98,9 +98,10 @@ struct Lane {
   const NfaArgs& A;
   Q& q;
   uint32_t key;
-  uint64_t base;
-  uint32_t n_ev = 0;  // events of the key
-  uint32_t j = 0;     // current event (sequence number within the key)
+  uint64_t base;      // CSR position of sequence number 0 (base + j = event j's position)
+  uint32_t j0 = 0;    // sequence number of the batch's first event of the key
+  uint32_t n_ev = 0;  // events of the key in this batch
+  uint32_t j = 0;     // current event (sequence number within the key's stream)
   EvT ev;             // fields of event ev_pos
   uint32_t ev_pos = CEP_NONE;
   v4u* rb;  // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
@@ -574,7 +575,7 @@ struct Lane {
     ocount = 0;
     // prefetch the next event's fields (consumed by the next event() call)
     EvT nev = ev;
-    const bool more = j + 1 < n_ev;
+    const bool more = j + 1 < j0 + n_ev;
     if (more) q.load_ev(nev, base + j + 1);
     const uint32_t n = count;
     for (uint32_t i = 0; i < n; i++) {
@@ -643,8 +644,8 @@ struct Lane {
   }
 
   __device__ __forceinline__ void run() {
-    const uint32_t n = n_ev;
-    uint32_t jj = 0;
+    const uint32_t n = j0 + n_ev;
+    uint32_t jj = j0;
     int pa_err = KE_OK;  // an exception of the per-event step (walks queued before it go first)
     uint32_t pa_seq = 0;
     while (jj < n) {
@@ -692,7 +693,8 @@ struct Lane {
   }
 };
 
-// Driver shared by the AOT and JIT kernels: slot -> key, initial state, stream, KeyState.
+// Driver shared by the AOT and JIT kernels: slot -> key, initial or carried state, the
+// batch's events of the key, KeyState (and KeyCarry for the next batch of a stream).
 template <int F, class Q>
 __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -701,32 +703,68 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
   const uint32_t key = A.key_list ? A.key_list[slot] : (uint32_t)slot;
   Lane<F, Q> L(A, q);
   L.key = key;
-  L.base = A.key_off[key];
-  L.n_ev = (uint32_t)(A.key_off[key + 1] - L.base);
+  L.n_ev = (uint32_t)(A.key_off[key + 1] - A.key_off[key]);
   L.rb = reinterpret_cast<v4u*>(A.rings) +
          (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (slot % 64);
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
-  // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
-  L.bdig = 1;
-  L.half = 0;
-  L.count = 0;
-  if (!Lane<F, Q>::kBeginReg) {
-    Dewey v;
-    dw_init(v, 1);
-    L.ocount = 0;
-    L.half = 1;  // push_rec writes the other half: half 0
-    L.readd_begin(q.begin_stage, v);
-    L.half = 0;
-    L.count = 1;
-  }
-  L.run();
   KeyState& ks = A.ks[key];
+  KeyCarry* kc = A.carry ? A.carry + key : nullptr;
+  if (kc && kc->live) {  // the key's NFA as the previous batch left it
+    if (kc->err) {        // stopped by an exception: stays stopped
+      ks.n_matches = ks.n_pairs = 0;
+      ks.out_first = CEP_NONE;
+      ks.err = kc->err;
+      ks.err_seq = kc->err_seq;
+      return;
+    }
+    L.j0 = kc->seq;
+    L.half = kc->half;
+    L.count = kc->count;
+    L.bdig = kc->bdig;
+    L.cur_first = kc->cur_first;
+    L.ncur = kc->ncur;
+    L.nend = kc->nend;
+    L.pcur = kc->pcur;
+    L.pend = kc->pend;
+    L.opc = kc->opc;
+  } else {
+    // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
+    L.bdig = 1;
+    L.half = 0;
+    L.count = 0;
+    if (!Lane<F, Q>::kBeginReg) {
+      Dewey v;
+      dw_init(v, 1);
+      L.ocount = 0;
+      L.half = 1;  // push_rec writes the other half: half 0
+      L.readd_begin(q.begin_stage, v);
+      L.half = 0;
+      L.count = 1;
+    }
+  }
+  L.base = A.key_off[key] - L.j0;
+  L.run();
   ks.n_matches = L.n_matches;
   ks.n_pairs = L.n_pairs;
   ks.out_first = L.out_first;
   ks.err = L.err;
   ks.err_seq = L.err_seq;
   if (L.err == KE_CAPACITY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
+  if (kc) {
+    kc->live = 1;
+    kc->seq = L.j0 + L.n_ev;
+    kc->half = L.half;
+    kc->count = L.count;
+    kc->bdig = L.bdig;
+    kc->cur_first = L.cur_first;
+    kc->ncur = L.ncur;
+    kc->nend = L.nend;
+    kc->pcur = L.pcur;
+    kc->pend = L.pend;
+    kc->opc = L.opc;
+    kc->err = L.err;
+    kc->err_seq = L.err_seq;
+  }
 }
 
 }  // namespace cep

@@ -75,6 +75,15 @@ template <class T> struct HVec {  // host copy of a result array
   std::vector<T> v;
 };
 
+// A streaming session's per-query NFA state (cep_opts.streaming): every key's run queue,
+// buffer pools and carried lane state persist from one batch to the next.
+struct StreamState {
+  DBuf rings, nodes, preds, carry, tops;  // tops: {node_top, pred_top} (device)
+  uint64_t n_keys = 0, node_cap = 0, pred_cap = 0;
+  uint32_t node_used = 0, pred_used = 0;  // pool tops after the last batch
+  bool init = false;
+};
+
 struct QueryRt {
   const cep_query* q;
   int F = 2;
@@ -101,6 +110,7 @@ struct QueryRt {
   float kernel_ms = 0;  // the matching kernel (nfa_kernel / stencil_kernel) launches
   float aux_ms = 0;     // setup and compaction kernels of the same batch
   uint32_t launches = 0;
+  StreamState st;
 };
 
 }  // namespace
@@ -252,6 +262,38 @@ void run_nfa(cep_session* s, QueryRt& r) {
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
+  const bool streaming = s->opts.streaming != 0;
+  StreamState& S = r.st;
+  if (streaming) {
+    if (!S.init) {
+      S.n_keys = nk;
+      S.carry.ensure(sizeof(KeyCarry) * std::max<uint64_t>(nk, 1));
+      HIPCHECK(hipMemsetAsync(S.carry.p, 0, sizeof(KeyCarry) * std::max<uint64_t>(nk, 1), s->stream));
+      S.tops.ensure(2 * sizeof(uint32_t));
+      HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
+      S.rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
+      S.init = true;
+    } else if (nk != S.n_keys) {
+      throw std::invalid_argument("the batches of a streaming session share one key space (n_keys)");
+    }
+    // a stream cannot re-run a key (its state moved on): size the pools for this batch on top
+    // of what the stream already holds, generously (capacity errors would be final)
+    const uint64_t add = s->n_events + nk * 2 * nchunk + 4096;
+    const uint64_t nn = std::min<uint64_t>(S.node_used + add, 0xFFFFFFF0ull);
+    const uint64_t pn = std::min<uint64_t>(S.pred_used + add, 0xFFFFFFF0ull);
+    if (nn > S.node_cap) {
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), 0xFFFFFFF0ull);
+      S.nodes.grow_keep(sizeof(Node) * c, sizeof(Node) * S.node_used, s->stream);
+      S.node_cap = c;
+    }
+    if (pn > S.pred_cap) {
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(pn, S.pred_cap * 3 / 2), 0xFFFFFFF0ull);
+      S.preds.grow_keep(sizeof(Pred) * c, sizeof(Pred) * S.pred_used, s->stream);
+      S.pred_cap = c;
+    }
+    out_cap = std::max<uint64_t>(out_cap, std::min<uint64_t>(nk + s->n_events / 64 + 1024, 0xFFFFFFF0ull / kOutChunkWords));
+    s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
+  }
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.n_keys = nk;
@@ -273,6 +315,15 @@ void run_nfa(cep_session* s, QueryRt& r) {
   a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, 1};
   a.ks = r.ks.as<KeyState>();
   a.n_capacity_err = &sc->n_cap_err;
+  if (streaming) {  // walks in place: a conflict could not be re-run (nfa_lane.h)
+    a.defer = 0;
+    a.rings = S.rings.p;
+    a.nodes = S.nodes.as<Node>();
+    a.preds = S.preds.as<Pred>();
+    a.carry = S.carry.as<KeyCarry>();
+    a.node_pool = Pool{S.tops.as<uint32_t>(), (uint32_t)S.node_cap, nchunk};
+    a.pred_pool = Pool{S.tops.as<uint32_t>() + 1, (uint32_t)S.pred_cap, pchunk};
+  }
 
   float total_ms = 0;
   r.launches = 0;
@@ -286,6 +337,13 @@ void run_nfa(cep_session* s, QueryRt& r) {
   float ms = 0;
   HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   total_ms += ms;
+  if (streaming) {  // no re-runs: a key that hit a limit keeps its error (sticky, reported)
+    uint32_t tops[2];
+    HIPCHECK(hipMemcpy(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost));
+    S.node_used = (uint32_t)std::min<uint64_t>(tops[0], S.node_cap);
+    S.pred_used = (uint32_t)std::min<uint64_t>(tops[1], S.pred_cap);
+    h.n_cap_err = 0;
+  }
 
   // retry keys that hit a capacity limit with 8x the live-run ring and grown pools, and
   // keys whose deferred walks conflicted (KE_CONFLICT), with walks in place
@@ -460,7 +518,7 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
       r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());
       HIPCHECK(hipMemcpy(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
                          hipMemcpyHostToDevice));
-      const bool nfa = queries[i]->info.kind == CEP_KIND_NFA || s->opts.force_nfa;
+      const bool nfa = queries[i]->info.kind == CEP_KIND_NFA || s->opts.force_nfa || s->opts.streaming;
       if (nfa && s->opts.tier == CEP_TIER_JIT) {  // the query's own kernel, compiled by hipRTC
         std::vector<char> co = jit_code_object(queries[i]->jitSource, &r->jit_compile_s);
         HIPCHECK(hipModuleLoadData(&r->mod, co.data()));
@@ -539,7 +597,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       s->watermark = (int64_t)(w ^ 0x8000000000000000ull);
     }
     for (auto& r : s->qs) {
-      if (r->q->info.kind == CEP_KIND_STENCIL && !s->opts.force_nfa) run_stencil(s, *r);
+      // a stream carries NFA state between batches: stencil queries run on the NFA there
+      if (r->q->info.kind == CEP_KIND_STENCIL && !s->opts.force_nfa && !s->opts.streaming) run_stencil(s, *r);
       else run_nfa(s, *r);
       r->have = true;
     }

@@ -166,7 +166,6 @@ struct StEval {
 template <int M, bool RANGE, int NCOL>
 __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   constexpr int H = M - 1;              // events a window reaches back
-  constexpr int D = NCOL > 1 ? 8 : 16;  // steps whose loads are issued together
   __shared__ uint32_t s_cnt[kStThreads / 64];
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
   // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs

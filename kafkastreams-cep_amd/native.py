@@ -36,7 +36,7 @@ class QueryInfo(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("device", C.c_int), ("force_nfa", C.c_int), ("tier", C.c_int), ("max_runs", C.c_uint32),
-                ("pool_factor", C.c_double)]
+                ("pool_factor", C.c_double), ("streaming", C.c_int)]
 
 
 class Batch(C.Structure):
@@ -206,12 +206,12 @@ class Session:
     """cep_session: per-key NFA state for one or more queries on one GPU."""
 
     def __init__(self, queries, device: int = 0, force_nfa: bool = False, max_runs: int = 0,
-                 pool_factor: float = 0.0, tier: int = CEP_TIER_JIT):
+                 pool_factor: float = 0.0, tier: int = CEP_TIER_JIT, streaming: bool = False):
         if isinstance(queries, Query):
             queries = [queries]
         self.queries = list(queries)
         arr = (C.c_void_p * len(self.queries))(*[q.h.value for q in self.queries])
-        opts = Opts(device, 1 if force_nfa else 0, tier, max_runs, pool_factor)
+        opts = Opts(device, 1 if force_nfa else 0, tier, max_runs, pool_factor, 1 if streaming else 0)
         h = C.c_void_p()
         _check(lib().cep_session_create(arr, len(self.queries), C.byref(opts), C.byref(h)))
         self.h = h

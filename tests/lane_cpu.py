@@ -49,7 +49,7 @@ def build(ir: bytes):
         os.replace(tmp, so)
     lib = C.CDLL(so)
     lib.lane_run.argtypes = [C.c_uint64, C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_void_p,
-                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]
+                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_int]
     lib.lane_n_matches.restype = C.c_uint64
     lib.lane_n_pairs.restype = C.c_uint64
     lib.lane_fetch.argtypes = [C.c_void_p] * 7
@@ -57,15 +57,19 @@ def build(ir: bytes):
     return lib
 
 
-def run(ir, key_off, cols, rcap=32, defer=True):
-    """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest)."""
+def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True):
+    """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
+    the batch continues the keys' streams of the previous streaming call (reset=False)."""
     lib = build(ir)
+    if streaming and reset:
+        lib.lane_stream_reset()
     key_off = np.ascontiguousarray(key_off, np.uint64)
     cols = [np.ascontiguousarray(c) for c in cols]
     ptrs = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
     nk = len(key_off) - 1
     retried = C.c_uint32()
-    lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried))
+    lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried),
+                 1 if streaming else 0)
     nm, npairs = lib.lane_n_matches(), lib.lane_n_pairs()
     key = np.zeros(nm, np.uint32)
     emit = np.zeros(nm, np.uint32)

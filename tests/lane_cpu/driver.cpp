@@ -28,13 +28,40 @@ static void on_fault(int sig) {  // a lane bug: print where, then die
   _exit(128 + sig);
 }
 
+// a streaming session's state between lane_run calls (streaming != 0)
+struct Stream {
+  std::vector<cep::Node> nodes;
+  std::vector<cep::Pred> preds;
+  std::vector<cep::KeyCarry> carry;
+  std::vector<cep::v4u> rings;
+  uint32_t node_top = 0, pred_top = 0;
+};
+static Stream g_stream;
+
+extern "C" void lane_stream_reset() { g_stream = Stream{}; }
+
 extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const* cols, int n_cols,
-                        const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried) {
+                        const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried, int streaming) {
   using namespace cep;
   signal(SIGSEGV, on_fault);
   const uint64_t ne = key_off[nk];
-  std::vector<Node> nodes(ne * 4 + nk * 64 + 4096);
-  std::vector<Pred> preds(ne * 4 + nk * 64 + 4096);
+  std::vector<Node> nodes_batch, *nodes_p = &nodes_batch;
+  std::vector<Pred> preds_batch, *preds_p = &preds_batch;
+  if (streaming) {  // pools persist; a fixed generous size for the tests' streams
+    if (g_stream.carry.empty()) {
+      g_stream.carry.assign(nk, KeyCarry{});
+      g_stream.nodes.resize(1 << 20);
+      g_stream.preds.resize(1 << 20);
+      g_stream.rings.resize(ring_bytes(8, nk, rcap) / 16 + 64);
+    }
+    nodes_p = &g_stream.nodes;
+    preds_p = &g_stream.preds;
+  } else {
+    nodes_batch.resize(ne * 4 + nk * 64 + 4096);
+    preds_batch.resize(ne * 4 + nk * 64 + 4096);
+  }
+  std::vector<Node>& nodes = *nodes_p;
+  std::vector<Pred>& preds = *preds_p;
   std::vector<uint32_t> out((ne + nk * 4 + 64) * 2 * kOutChunkWords);
   std::vector<KeyState> ks(nk);
   // device pools are not cleared between batches: start from garbage, not zeros
@@ -45,8 +72,10 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       std::memcpy((char*)p + i, &x, 8);
     }
   };
-  scribble(nodes.data(), nodes.size() * sizeof(Node));
-  scribble(preds.data(), preds.size() * sizeof(Pred));
+  if (!streaming) {
+    scribble(nodes.data(), nodes.size() * sizeof(Node));
+    scribble(preds.data(), preds.size() * sizeof(Pred));
+  }
   scribble(out.data(), out.size() * 4);
   uint32_t node_top = 0, pred_top = 0, out_top = 0, n_cap = 0;
   NfaArgs a{};
@@ -57,17 +86,21 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   a.nodes = nodes.data();
   a.preds = preds.data();
   a.out = out.data();
-  a.node_pool = Pool{&node_top, (uint32_t)nodes.size(), 16};
-  a.pred_pool = Pool{&pred_top, (uint32_t)preds.size(), 16};
+  a.node_pool = Pool{streaming ? &g_stream.node_top : &node_top, (uint32_t)nodes.size(), 16};
+  a.pred_pool = Pool{streaming ? &g_stream.pred_top : &pred_top, (uint32_t)preds.size(), 16};
+  if (streaming) a.carry = g_stream.carry.data();
   a.out_pool = Pool{&out_top, (uint32_t)(out.size() / kOutChunkWords), 1};
   a.ks = ks.data();
   a.n_capacity_err = &n_cap;
   auto launch = [&](uint64_t nslots, uint32_t rc, int df) {
-    std::vector<v4u> rings(ring_bytes(8, nslots, rc) / 16 + 64);
+    std::vector<v4u> rings_batch;
+    if (!streaming) {
+      rings_batch.resize(ring_bytes(8, nslots, rc) / 16 + 64);
+      scribble(rings_batch.data(), rings_batch.size() * 16);
+    }
     std::vector<v4u> walks(walkq_bytes(nslots, 32) / 16 + 64);
-    scribble(rings.data(), rings.size() * 16);
     scribble(walks.data(), walks.size() * 16);
-    a.rings = rings.data();
+    a.rings = streaming ? g_stream.rings.data() : rings_batch.data();
     a.rcap = rc;
     a.walks = walks.data();
     a.wcap = 32;
@@ -79,9 +112,9 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       cep_nfa_jit(a);
     }
   };
-  launch(nk, rcap, defer);
+  launch(nk, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
   *n_retried = 0;
-  for (int round = 0; n_cap > 0 && round < 3; round++) {  // session.cpp run_nfa
+  for (int round = 0; !streaming && n_cap > 0 && round < 3; round++) {  // session.cpp run_nfa
     std::vector<uint32_t> list;
     for (uint64_t k = 0; k < nk; k++)
       if (ks[k].err == KE_CAPACITY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);

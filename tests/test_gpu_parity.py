@@ -230,3 +230,34 @@ def test_pool_growth_tiny_pools():
     ir = W.stock_query("readme").to_ir()
     s = N.Session(N.Query(ir), pool_factor=0.001)
     assert_parity(gpu_run(ir, off, cols, session=s), oracle.run(ir, off, cols, threads=8), off)
+
+
+@pytest.mark.parametrize("tier", TIERS)
+@pytest.mark.parametrize("query,n_batches", [("readme", 3), ("test", 5), ("any_kleene", 3), ("strict", 4)])
+def test_streaming_session_batches(query, n_batches, tier):
+    """cep_opts.streaming: the stream cut into consecutive batches per key gives, per key, the
+    oracle's single-pass matches (global sequence numbers) and exceptions."""
+    import stream_split as SS
+    kind = "abc" if query == "strict" else "stock"
+    cfg = W.SynthConfig("t", kind, 400, 700, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    q = {"readme": lambda: W.stock_query("readme"), "test": lambda: W.stock_query("test"),
+         "any_kleene": W.any_kleene_query, "strict": W.strict_abc_query}[query]()
+    ir = q.to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    s = N.Session(N.Query(ir), streaming=True, tier=tier, max_runs=64)
+    outs = []
+    for ko, cs in SS.split(off, cols, n_batches, seed=n_batches):
+        s.push(ko, cs)
+        m = s.matches(0)
+        m["err_code"], m["err_seq"] = s.key_errors(0)
+        outs.append(m)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
+def test_streaming_rejects_other_key_space():
+    s = N.Session(N.Query(W.stock_query("readme").to_ir()), streaming=True)
+    s.push(np.array([0, 2], np.uint64), [np.array([1, 2], np.int32), np.array([1, 2], np.int32)])
+    with pytest.raises(N.CepError):
+        s.push(np.array([0, 1, 2], np.uint64), [np.array([1, 2], np.int32), np.array([1, 2], np.int32)])

@@ -60,3 +60,40 @@ def test_lane_fuzz(seed):
     r = oracle.run(ir, off, cols)
     lane_cpu.assert_same(lane_cpu.run(ir, off, cols), r, off)
     lane_cpu.assert_same(lane_cpu.run(ir, off, cols, defer=False), r, off)
+
+
+@pytest.mark.parametrize("query,n_batches", [("readme", 3), ("test", 4), ("any_kleene", 3), ("strict", 5)])
+def test_lane_streaming_batches(query, n_batches):
+    """A streaming session fed the stream in consecutive pieces per key produces, per key, the
+    same matches (global sequence numbers) and errors as the whole stream in one pass."""
+    import stream_split as SS
+    cfg = W.SynthConfig("t", "abc" if query == "strict" else "stock", 60, 500, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    q = {"readme": lambda: W.stock_query("readme"), "test": lambda: W.stock_query("test"),
+         "any_kleene": W.any_kleene_query, "strict": W.strict_abc_query}[query]()
+    ir = q.to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    batches = SS.split(off, cols, n_batches, seed=n_batches)
+    outs = [lane_cpu.run(ir, ko, cs, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    last = outs[-1]
+    np.testing.assert_array_equal(last["err_code"], r["err_code"])
+    bad = r["err_code"] != 0
+    np.testing.assert_array_equal(last["err_seq"][bad].astype(np.uint64),
+                                  r["err_pos"][bad].astype(np.uint64) - np.asarray(off, np.uint64)[:-1][bad])
+
+
+@pytest.mark.parametrize("seed", range(3, 160, 16))
+def test_lane_streaming_fuzz(seed):
+    import stream_split as SS
+    q = random_query(seed)
+    ir = q.to_ir()
+    if oracle.compile_check(ir):
+        pytest.skip("reference compile-time exception")
+    off, cols = random_stream(seed, 60, 14)
+    r = oracle.run(ir, off, cols)
+    batches = SS.split(off, cols, 3, seed=seed)
+    # a stream cannot re-run a key that outgrows its run queue: size it like the retries would
+    outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
