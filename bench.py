@@ -166,6 +166,40 @@ def secondary_strict(device, steps, warmup, dist):
     return res
 
 
+def end_to_end(args, device, dist):
+    """SURVEY §8(d)'s secondary figure: the same cfg-3 workload handed over in arrival order
+    (a key id per event, round-robin interleaved), so each step includes the device partition
+    (stable radix sort by key + column gather, csrc/partition.hip) before the NFA."""
+    cfg = W.CONFIGS[3]
+    st = N.synth_arrival_stream("stock", cfg.seed, args.keys, args.mean, dist.rank * args.keys, device)
+    q = N.Query(W.stock_query(args.variant).to_ir())
+    s = N.Session(q, device=device)
+    for _ in range(max(1, args.warmup)):
+        s.push_arrival_device(st)
+    part, kern = [], []
+    dist.barrier()
+    N.lib().cep_sync(s.h)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s.push_arrival_device(st)
+        part.append(_partition_ms(s))
+        kern.append(s.timing(0)[0])
+    N.lib().cep_sync(s.h)
+    el = time.perf_counter() - t0
+    n_m, _ = s.digest(0)
+    s.close()
+    return {"workload": "cfg3 stock query, arrival-order batches (partition on the GPU + NFA)",
+            "value": st.n_events * args.steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / args.steps,
+            "partition_ms": float(np.mean(part)), "nfa_kernel_ms": float(np.mean(kern)),
+            "matches_per_step": n_m}
+
+
+def _partition_ms(s):
+    off, perm, ms = N.C.c_void_p(), N.C.c_void_p(), N.C.c_double()
+    N._check(N.lib().cep_batch_layout(s.h, N.CEP_MEM_DEVICE, N.C.byref(off), N.C.byref(perm), N.C.byref(ms)))
+    return ms.value
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,6 +212,7 @@ def main():
     ap.add_argument("--cpu-every", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the arrival-order end-to-end figure")
     args = ap.parse_args()
 
     dist = Dist()
@@ -236,6 +271,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(cfg, args.variant, args.cpu_threads, args.cpu_every)
         if dist.world == 1 and not args.no_secondary:
             out["secondary"] = secondary_strict(device, args.steps, args.warmup, dist)
+        if dist.world == 1 and not args.no_e2e:
+            sess.close()
+            out["end_to_end"] = end_to_end(args, device, dist)
         print(json.dumps(out), flush=True)
     sess.close()
     dist.close()

@@ -141,10 +141,15 @@ void cep_session_destroy(cep_session* s);
 typedef struct {
   uint64_t n_keys;
   uint64_t n_events;
-  const uint64_t* key_off;  /* [n_keys + 1] */
+  const uint64_t* key_off;  /* [n_keys + 1] (NULL for an arrival-order batch) */
   const void* const* cols;  /* [n_fields] */
   const int64_t* ts;        /* [n_events] or NULL */
   int memory;               /* CEP_MEM_HOST or CEP_MEM_DEVICE */
+  /* Arrival-order batch: instead of key_off, the key (< n_keys) of every event, the events
+   * and cols/ts in the order the records arrived (a run of CEPProcessor.process calls).  The
+   * batch is partitioned on the device (stable: each key keeps its arrival order);
+   * cep_batch_layout gives the resulting CSR layout and the arrival index of each position. */
+  const uint32_t* arrival_key;  /* [n_events] or NULL */
 } cep_batch;
 
 /* Runs every query of the session over the batch: a run of process() calls per key.  In a
@@ -156,6 +161,13 @@ typedef struct {
  * stencil-kind queries run on the NFA kernel.  Returns once the batch's kernels have
  * completed (buffers are borrowed for the call only). */
 int cep_push_batch(cep_session* s, const cep_batch* b);
+
+/* Layout of the last batch as the matchers saw it: key_off [n_keys + 1] and, for an
+ * arrival-order batch, arrival_index [n_events] (the arrival position of each CSR position;
+ * NULL for a CSR batch).  Arrays live in `memory` space until the next push/destroy.
+ * partition_ms: device time of the partition (0 for a CSR batch). */
+int cep_batch_layout(cep_session* s, int memory, const uint64_t** key_off, const uint32_t** arrival_index,
+                     double* partition_ms);
 int cep_sync(cep_session* s);
 
 /* Matches of query `query` for the last batch, ordered by key then emission order (the
@@ -214,6 +226,10 @@ int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64
                     uint32_t mean_events, uint64_t* n_events);
 int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
                        uint32_t mean_events, uint64_t* key_off_dev, int32_t* const* cols_dev);
+/* The same stream in arrival order (round robin: ordered by (index within key, key)): the key
+ * of every event in keys_dev [n_events], values in cols_dev. */
+int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
+                               uint32_t mean_events, uint32_t* keys_dev, int32_t* const* cols_dev);
 
 #ifdef __cplusplus
 }

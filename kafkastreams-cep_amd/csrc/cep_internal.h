@@ -52,6 +52,14 @@ hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_b
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
 uint64_t synth_hash_host(uint64_t seed, uint64_t key, uint64_t j);
 std::vector<char> jit_code_object(const std::string& src, double* compile_s);
+struct Cols;
+size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
+hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
+                     const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
+                     uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
+                     hipStream_t st);
+hipError_t csr_to_arrival(const uint64_t* key_off, uint64_t n_keys, uint64_t n, uint64_t max_nk, const int32_t* c0,
+                          const int32_t* c1, uint32_t* key_out, int32_t* o0, int32_t* o1, hipStream_t st);
 std::string jit_cache_key(const std::string& src);
 
 }  // namespace cep

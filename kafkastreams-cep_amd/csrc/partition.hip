@@ -1,0 +1,148 @@
+// partition.hip — arrival-order batches -> the key-partitioned (CSR) layout the matchers read.
+//
+// The reference's processor receives records one at a time in arrival order
+// (CEPProcessor.process, CEPProcessor.java:155-163) and each key's NFA sees that key's records
+// in that order.  A batch handed over in arrival order (one key id per event) is
+// partitioned on the device: a stable LSD radix sort of (key, arrival index) pairs by key
+// (rocPRIM through hipCUB), key counts -> key_off (exclusive scan), then one gather per column.
+// Stability is what keeps every key's events in arrival order.  All passes are HBM-bound.
+//
+// Also the synthetic arrival-order stream of the bench/tests: the CSR stream of
+// workloads.generate interleaved round-robin, arrival order = (index within key, key).
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "kernel_args.h"
+
+namespace cep {
+
+__global__ void __launch_bounds__(256) iota_u32(uint32_t* v, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+// counts per key (atomics; the order of the adds does not matter) and a range check
+__global__ void __launch_bounds__(256) count_keys(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_keys,
+                                                  unsigned long long* cnt, unsigned* bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = key[i];
+  if (k >= n_keys) {
+    atomicOr(bad, 1u);
+    return;
+  }
+  atomicAdd(cnt + k, 1ull);
+}
+
+// CSR position p <- arrival index perm[p], for every column (4- or 8-byte values) and ts
+__global__ void __launch_bounds__(256) gather_cols(const uint32_t* __restrict__ perm, uint64_t n, int nf, Cols in,
+                                                   Cols out, uint32_t wide_mask, const int64_t* ts_in,
+                                                   int64_t* ts_out) {
+  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t src = perm[p];
+  for (int f = 0; f < nf; f++) {
+    if ((wide_mask >> f) & 1u)
+      ((int64_t*)out.p[f])[p] = ((const int64_t*)in.p[f])[src];
+    else
+      ((int32_t*)out.p[f])[p] = ((const int32_t*)in.p[f])[src];
+  }
+  if (ts_in) ts_out[p] = ts_in[src];
+}
+
+static int key_bits(uint64_t n_keys) {
+  int b = 1;
+  while (b < 32 && (1ull << b) < n_keys) b++;
+  return b;
+}
+
+// Device scratch of partition(): bytes needed for n events over n_keys keys.
+size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys) {
+  size_t tmp = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1));
+  size_t scan = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                   (int)(n_keys + 1));
+  return std::max(tmp, scan) + 256;
+}
+
+// arrival-order batch -> key_off[n_keys + 1], perm[n] (arrival index of each CSR position),
+// columns in CSR order.  scratch: partition_scratch_bytes; sorted_keys, idx: n u32 each.
+hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
+                     const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
+                     uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
+                     hipStream_t st) {
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (n_keys + 1), st);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  if (n) {
+    hipLaunchKernelGGL(iota_u32, dim3(blocks), dim3(256), 0, st, idx, n);
+    hipLaunchKernelGGL(count_keys, dim3(blocks), dim3(256), 0, st, key, n, n_keys, (unsigned long long*)cnt, bad);
+  }
+  size_t tmp = scratch_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(scratch, tmp, (unsigned long long*)cnt, (unsigned long long*)key_off,
+                                       (int)(n_keys + 1), st);
+  if (e != hipSuccess || n == 0) return e;
+  if (e != hipSuccess) return e;
+  tmp = scratch_bytes;
+  e = hipcub::DeviceRadixSort::SortPairs(scratch, tmp, key, sorted_keys, idx, perm, (int)n, 0, key_bits(n_keys), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gather_cols, dim3(blocks), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in, ts_out);
+  return hipGetLastError();
+}
+
+// ---- synthetic arrival order: CSR position p of key k, index j -> sort key j * n_keys + k
+__global__ void __launch_bounds__(256) arrival_keys(const uint64_t* __restrict__ key_off, uint64_t n_keys,
+                                                    uint64_t* skey, uint32_t* kid) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_keys) return;
+  for (uint64_t p = key_off[k]; p < key_off[k + 1]; p++) {
+    skey[p] = (p - key_off[k]) * n_keys + k;
+    kid[p] = (uint32_t)k;
+  }
+}
+
+__global__ void __launch_bounds__(256) arrival_gather(const uint32_t* __restrict__ order, uint64_t n, const uint32_t* kid,
+                                                      const int32_t* c0, const int32_t* c1, uint32_t* key_out,
+                                                      int32_t* o0, int32_t* o1) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = order[i];
+  key_out[i] = kid[p];
+  o0[i] = c0[p];
+  if (c1) o1[i] = c1[p];
+}
+
+// CSR stream (key_off, c0, c1) -> arrival order (key_out, o0, o1), on the device
+hipError_t csr_to_arrival(const uint64_t* key_off, uint64_t n_keys, uint64_t n, uint64_t max_nk, const int32_t* c0,
+                          const int32_t* c1, uint32_t* key_out, int32_t* o0, int32_t* o1, hipStream_t st) {
+  if (n == 0 || n_keys == 0) return hipSuccess;
+  uint64_t *skey = nullptr, *skey2 = nullptr;
+  uint32_t *kid = nullptr, *idx = nullptr, *order = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  hipError_t e = hipSuccess;
+  auto ok = [&](hipError_t x) { if (e == hipSuccess) e = x; return e == hipSuccess; };
+  int bits = 1;  // sort keys < max_nk * n_keys
+  while (bits < 64 && (max_nk * n_keys) >> bits) bits++;
+  if (ok(hipMalloc(&skey, 8 * n)) && ok(hipMalloc(&skey2, 8 * n)) && ok(hipMalloc(&kid, 4 * n)) &&
+      ok(hipMalloc(&idx, 4 * n)) && ok(hipMalloc(&order, 4 * n))) {
+    hipLaunchKernelGGL(arrival_keys, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, skey, kid);
+    hipLaunchKernelGGL(iota_u32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, idx, n);
+    ok(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, skey, skey2, idx, order, (int)n, 0, bits, st));
+    if (ok(hipMalloc(&tmp, tmp_bytes + 256)) &&
+        ok(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, skey, skey2, idx, order, (int)n, 0, bits, st))) {
+      hipLaunchKernelGGL(arrival_gather, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, order, n, kid, c0, c1,
+                         key_out, o0, o1);
+      ok(hipGetLastError());
+      ok(hipStreamSynchronize(st));
+    }
+  }
+  for (void* p : {(void*)skey, (void*)skey2, (void*)kid, (void*)idx, (void*)order, tmp})
+    if (p) (void)hipFree(p);
+  return e;
+}
+
+}  // namespace cep

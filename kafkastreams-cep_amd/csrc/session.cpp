@@ -129,6 +129,14 @@ struct cep_session {
   const int64_t* ts = nullptr;
   Cols cols{};
   int64_t watermark = INT64_MIN;
+  // arrival-order batches: device copies of the input, the partitioned (CSR) batch
+  DBuf a_keys, a_ts, p_off, p_cnt, p_ts, p_perm, p_sorted, p_idx, p_scratch;
+  DBuf a_cols[kMaxFields], p_cols[kMaxFields];
+  bool arrival = false;
+  float partition_ms = 0;
+  std::vector<uint64_t> h_off;
+  std::vector<uint32_t> h_perm;
+  bool layout_host_valid = false;
   // scratch
   DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask;
 };
@@ -546,8 +554,68 @@ void cep_session_destroy(cep_session* s) {
   delete s;
 }
 
+// arrival-order batch -> s->key_off / s->cols / s->ts in CSR order (partition.hip)
+static void partition_batch(cep_session* s, const cep_batch* b) {
+  const cep_query* q0 = s->qs[0]->q;
+  const uint32_t nf = q0->info.n_fields;
+  const uint64_t n = b->n_events, nk = b->n_keys;
+  const uint32_t* keys = b->arrival_key;
+  Cols in{}, out{};
+  const int64_t* ts = b->ts;
+  uint32_t wide = 0;
+  for (uint32_t f = 0; f < nf; f++) wide |= (q0->dev.field_type[f] == 1 ? 0u : 1u) << f;
+  if (b->memory != CEP_MEM_DEVICE) {
+    s->a_keys.ensure(4 * std::max<uint64_t>(n, 1));
+    if (n) HIPCHECK(hipMemcpyAsync(s->a_keys.p, keys, 4 * n, hipMemcpyHostToDevice, s->stream));
+    keys = s->a_keys.as<uint32_t>();
+    for (uint32_t f = 0; f < nf; f++) {
+      const size_t esz = (wide >> f) & 1u ? 8 : 4;
+      s->a_cols[f].ensure(esz * std::max<uint64_t>(n, 1));
+      if (n) HIPCHECK(hipMemcpyAsync(s->a_cols[f].p, b->cols[f], esz * n, hipMemcpyHostToDevice, s->stream));
+      in.p[f] = s->a_cols[f].p;
+    }
+    if (ts) {
+      s->a_ts.ensure(8 * std::max<uint64_t>(n, 1));
+      if (n) HIPCHECK(hipMemcpyAsync(s->a_ts.p, ts, 8 * n, hipMemcpyHostToDevice, s->stream));
+      ts = s->a_ts.as<int64_t>();
+    }
+  } else {
+    for (uint32_t f = 0; f < nf; f++) in.p[f] = b->cols[f];
+  }
+  for (uint32_t f = 0; f < nf; f++) {
+    s->p_cols[f].ensure(((wide >> f) & 1u ? 8 : 4) * std::max<uint64_t>(n, 1));
+    out.p[f] = s->p_cols[f].p;
+  }
+  if (ts) s->p_ts.ensure(8 * std::max<uint64_t>(n, 1));
+  s->p_off.ensure(8 * (nk + 1));
+  s->p_cnt.ensure(8 * (nk + 1));
+  s->p_perm.ensure(4 * std::max<uint64_t>(n, 1));
+  s->p_sorted.ensure(4 * std::max<uint64_t>(n, 1));
+  s->p_idx.ensure(4 * std::max<uint64_t>(n, 1));
+  const size_t sb = partition_scratch_bytes(n, nk);
+  s->p_scratch.ensure(sb);
+  s->scratch.ensure(sizeof(Scratch));
+  Scratch* sc = s->scratch.as<Scratch>();
+  HIPCHECK(hipMemsetAsync(&sc->overflow, 0, sizeof(uint32_t), s->stream));
+  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  HIPCHECK(partition(keys, n, nk, (int)nf, in, out, wide, ts, ts ? s->p_ts.as<int64_t>() : nullptr,
+                     s->p_off.as<uint64_t>(), s->p_cnt.as<uint64_t>(), s->p_perm.as<uint32_t>(),
+                     s->p_sorted.as<uint32_t>(), s->p_idx.as<uint32_t>(), s->p_scratch.p, sb, &sc->overflow,
+                     s->stream));
+  HIPCHECK(hipEventRecord(s->ev1, s->stream));
+  uint32_t bad = 0;
+  HIPCHECK(hipMemcpyAsync(&bad, &sc->overflow, sizeof bad, hipMemcpyDeviceToHost, s->stream));
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  HIPCHECK(hipEventElapsedTime(&s->partition_ms, s->ev0, s->ev1));
+  if (bad) throw std::invalid_argument("arrival_key: a key id >= n_keys");
+  s->key_off = s->p_off.as<uint64_t>();
+  s->cols = out;
+  s->ts = ts ? s->p_ts.as<int64_t>() : nullptr;
+}
+
 int cep_push_batch(cep_session* s, const cep_batch* b) {
-  if (!s || !b || !b->key_off || (!b->cols && b->n_events)) return fail(CEP_E_INVALID, "null argument");
+  if (!s || !b || (!b->key_off && !b->arrival_key) || (!b->cols && b->n_events))
+    return fail(CEP_E_INVALID, "null argument");
   if (b->n_keys >= 0xFFFFFFFFull || b->n_events >= 0xFFFFFFFFull)
     return fail(CEP_E_INVALID, "a batch holds < 2^32 keys and events (sequence numbers are u32)");
   return guarded([&] {
@@ -560,7 +628,12 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       r->have = false;
       r->host_valid = false;
     }
-    if (b->memory == CEP_MEM_DEVICE) {
+    s->arrival = b->arrival_key != nullptr;
+    s->partition_ms = 0;
+    s->layout_host_valid = false;
+    if (s->arrival) {
+      partition_batch(s, b);
+    } else if (b->memory == CEP_MEM_DEVICE) {
       s->key_off = b->key_off;
       for (uint32_t f = 0; f < nf; f++) s->cols.p[f] = b->cols[f];
       s->ts = b->ts;
@@ -602,6 +675,32 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       else run_nfa(s, *r);
       r->have = true;
     }
+  });
+}
+
+int cep_batch_layout(cep_session* s, int memory, const uint64_t** key_off, const uint32_t** arrival_index,
+                     double* partition_ms) {
+  if (!s) return fail(CEP_E_INVALID, "null session");
+  if (!s->key_off) return fail(CEP_E_STATE, "no batch has been pushed");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    if (partition_ms) *partition_ms = s->partition_ms;
+    if (memory == CEP_MEM_DEVICE) {
+      if (key_off) *key_off = s->key_off;
+      if (arrival_index) *arrival_index = s->arrival ? s->p_perm.as<uint32_t>() : nullptr;
+      return;
+    }
+    if (!s->layout_host_valid) {
+      s->h_off.resize(s->n_keys + 1);
+      HIPCHECK(hipMemcpyAsync(s->h_off.data(), s->key_off, 8 * (s->n_keys + 1), hipMemcpyDeviceToHost, s->stream));
+      s->h_perm.resize(s->arrival ? s->n_events : 0);
+      if (s->arrival && s->n_events)
+        HIPCHECK(hipMemcpyAsync(s->h_perm.data(), s->p_perm.p, 4 * s->n_events, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipStreamSynchronize(s->stream));
+      s->layout_host_valid = true;
+    }
+    if (key_off) *key_off = s->h_off.data();
+    if (arrival_index) *arrival_index = s->arrival ? s->h_perm.data() : nullptr;
   });
 }
 
@@ -779,6 +878,31 @@ int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uin
     HIPCHECK(hipMemcpy(key_off_dev, off.data(), sizeof(uint64_t) * (n_keys + 1), hipMemcpyHostToDevice));
     HIPCHECK(launch_synth(kind, seed, n_keys, key_base, key_off_dev, cols_dev[0], kind == 1 ? cols_dev[1] : nullptr,
                           nullptr));
+    HIPCHECK(hipDeviceSynchronize());
+  });
+}
+
+int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
+                               uint32_t mean_events, uint32_t* keys_dev, int32_t* const* cols_dev) {
+  if (!keys_dev || !cols_dev || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
+  if (kind != 0 && kind != 1) return fail(CEP_E_INVALID, "kind must be 0 (abc) or 1 (stock)");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    auto off = synth_offsets(kind, seed, n_keys, key_base, mean_events);
+    const uint64_t n = off[n_keys];
+    uint64_t max_nk = 1;
+    for (uint64_t k = 0; k < n_keys; k++) max_nk = std::max<uint64_t>(max_nk, off[k + 1] - off[k]);
+    DBuf d_off, c0, c1;
+    d_off.ensure(8 * (n_keys + 1));
+    c0.ensure(4 * std::max<uint64_t>(n, 1));
+    if (kind == 1) c1.ensure(4 * std::max<uint64_t>(n, 1));
+    HIPCHECK(hipMemcpy(d_off.p, off.data(), 8 * (n_keys + 1), hipMemcpyHostToDevice));
+    HIPCHECK(launch_synth(kind, seed, n_keys, key_base, d_off.as<uint64_t>(), c0.as<int32_t>(),
+                          kind == 1 ? c1.as<int32_t>() : nullptr, nullptr));
+    HIPCHECK(csr_to_arrival(d_off.as<uint64_t>(), n_keys, n, max_nk, c0.as<int32_t>(),
+                            kind == 1 ? c1.as<int32_t>() : nullptr, keys_dev, cols_dev[0],
+                            kind == 1 ? cols_dev[1] : nullptr, nullptr));
     HIPCHECK(hipDeviceSynchronize());
   });
 }

@@ -25,6 +25,7 @@ EXPORTS = [
     "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
+    "cep_batch_layout", "cep_synth_generate_arrival",
 ]
 
 
@@ -41,7 +42,8 @@ class Opts(C.Structure):
 
 class Batch(C.Structure):
     _fields_ = [("n_keys", C.c_uint64), ("n_events", C.c_uint64), ("key_off", C.c_void_p),
-                ("cols", C.POINTER(C.c_void_p)), ("ts", C.c_void_p), ("memory", C.c_int)]
+                ("cols", C.POINTER(C.c_void_p)), ("ts", C.c_void_p), ("memory", C.c_int),
+                ("arrival_key", C.c_void_p)]
 
 
 class Matches(C.Structure):
@@ -85,6 +87,8 @@ def lib():
             "cep_memcpy": ([vp, vp, C.c_size_t, C.c_int, C.c_int], C.c_int),
             "cep_synth_count": ([C.c_int, C.c_int, u64, u64, u64, u32, C.POINTER(u64)], C.c_int),
             "cep_synth_generate": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
+            "cep_synth_generate_arrival": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
+            "cep_batch_layout": ([vp, C.c_int, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_double)], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -202,6 +206,30 @@ def synth_stream(kind: str, seed: int, n_keys: int, mean_events: int, key_base: 
     return DeviceStream(n_keys, n.value, off, cols, device)
 
 
+class ArrivalStream:
+    """A device-resident arrival-order batch: the key of every event + int32 columns."""
+
+    def __init__(self, n_keys, n_events, keys: DeviceBuffer, cols: list, device=0):
+        self.n_keys, self.n_events = int(n_keys), int(n_events)
+        self.keys, self.cols, self.device = keys, cols, device
+
+    def download(self):
+        return self.keys.download(np.uint32, self.n_events), [c.download(np.int32, self.n_events) for c in self.cols]
+
+
+def synth_arrival_stream(kind: str, seed: int, n_keys: int, mean_events: int, key_base: int = 0,
+                         device: int = 0) -> ArrivalStream:
+    """workloads.generate_arrival's stream, generated in HBM (csrc/partition.hip)."""
+    k = {"abc": 0, "stock": 1}[kind]
+    n = C.c_uint64()
+    _check(lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
+    keys = DeviceBuffer(4 * max(1, n.value), device)
+    cols = [DeviceBuffer(4 * max(1, n.value), device) for _ in range(1 if k == 0 else 2)]
+    ptrs = (C.c_void_p * len(cols))(*[c.ptr for c in cols])
+    _check(lib().cep_synth_generate_arrival(device, k, seed, n_keys, key_base, mean_events, keys.ptr, ptrs))
+    return ArrivalStream(n_keys, n.value, keys, cols, device)
+
+
 class Session:
     """cep_session: per-key NFA state for one or more queries on one GPU."""
 
@@ -240,6 +268,35 @@ class Session:
                   ptrs, tsp, CEP_MEM_HOST)
         _check(lib().cep_push_batch(self.h, C.byref(b)))
         self.n_keys = len(key_off) - 1
+
+    def push_arrival(self, keys, cols, n_keys: int, ts=None):
+        """Host batch in arrival order: keys[i] is the key of event i (partitioned on the GPU)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        cols = [np.ascontiguousarray(c) for c in cols]
+        ptrs = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+        tsp = None
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, dtype=np.int64)
+            tsp = ts.ctypes.data
+        b = Batch(n_keys, len(keys), None, ptrs, tsp, CEP_MEM_HOST, keys.ctypes.data)
+        _check(lib().cep_push_batch(self.h, C.byref(b)))
+        self.n_keys = n_keys
+
+    def push_arrival_device(self, stream: ArrivalStream):
+        ptrs = (C.c_void_p * len(stream.cols))(*[c.ptr for c in stream.cols])
+        b = Batch(stream.n_keys, stream.n_events, None, ptrs, None, CEP_MEM_DEVICE, stream.keys.ptr)
+        _check(lib().cep_push_batch(self.h, C.byref(b)))
+        self.n_keys = stream.n_keys
+
+    def layout(self):
+        """(key_off, arrival_index or None, partition_ms) of the last batch (host copies)."""
+        off, perm, ms = C.c_void_p(), C.c_void_p(), C.c_double()
+        _check(lib().cep_batch_layout(self.h, CEP_MEM_HOST, C.byref(off), C.byref(perm), C.byref(ms)))
+        ko = np.ctypeslib.as_array(C.cast(off, C.POINTER(C.c_uint64)), shape=(self.n_keys + 1,)).copy()
+        ai = None
+        if perm.value:
+            ai = np.ctypeslib.as_array(C.cast(perm, C.POINTER(C.c_uint32)), shape=(int(ko[-1]),)).copy()
+        return ko, ai, ms.value
 
     def push_device(self, stream: DeviceStream, ts_ptr=None):
         ptrs = (C.c_void_p * len(stream.cols))(*[c.ptr for c in stream.cols])

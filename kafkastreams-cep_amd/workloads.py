@@ -160,6 +160,17 @@ def generate(cfg: SynthConfig, keys: np.ndarray | None = None):
     return key_off, [price.astype(np.int32), vol.astype(np.int32)]
 
 
+def generate_arrival(cfg: SynthConfig, keys: np.ndarray | None = None):
+    """The same stream in arrival order (round robin: by index within key, then key), as
+    csrc/partition.hip produces it.  Returns (key of each event u32, columns)."""
+    key_off, cols = generate(cfg, keys)
+    counts = np.diff(key_off.astype(np.int64))
+    kid = np.repeat(np.arange(len(counts), dtype=np.int64), counts)
+    j = np.arange(int(key_off[-1]), dtype=np.int64) - np.repeat(key_off[:-1].astype(np.int64), counts)
+    order = np.lexsort((kid, j))
+    return kid[order].astype(np.uint32), [c[order] for c in cols]
+
+
 # ------------------------------------------------------------------------------ digest
 def _mix64(z: np.ndarray) -> np.ndarray:
     with np.errstate(over="ignore"):
