@@ -11,6 +11,7 @@ parity tests proper.
 import ctypes as C
 import hashlib
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -26,7 +27,8 @@ _libs = {}
 
 def build(ir: bytes):
     """Compile the query's kernel for the host; returns the loaded library (cached)."""
-    src = N.Query(ir).jit_source
+    # the occupancy attribute is for the GPU compile only (the host has no kernels)
+    src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\d+\)\)\)", "", N.Query(ir).jit_source)
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
                    ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
