@@ -711,7 +711,24 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   std::string occ;
   if (waves > 0) occ = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))";
   o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256)" + occ + " cep_nfa_jit(NfaArgs A) {\n";
-  o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n}  // namespace cep\n";
+  o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n";
+  if (bpred) {
+    // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
+    // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
+    // One wave per key: the key's events are contiguous, so its loads coalesce.
+    o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_est(NfaArgs A) {\n";
+    o += "  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n  const uint32_t lane = threadIdx.x & 63;\n";
+    o += "  if (k >= A.n_keys) return;\n";
+    o += "  const uint64_t base = A.key_off[k];\n  const uint32_t n = (uint32_t)(A.key_off[k + 1] - base);\n";
+    o += "  uint64_t w = 0;\n  for (uint32_t j = lane; j < n; j += 64) {\n    Ev e;\n    ld_bev(e, A, base + j);\n";
+    o += "    Fo f;\n    f.nm = (1u << F) - 1;\n    int err = 0;\n";
+    o += "    const bool r = " + predName[d.begin_stage][0] + "(e, f, err);\n";
+    o += "    if (r || err) w += n - j;\n  }\n";
+    o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
+    o += "  w += n / kQuietChunk + 1;\n";
+    o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
+  }
+  o += "}  // namespace cep\n";
   return o;
 }
 

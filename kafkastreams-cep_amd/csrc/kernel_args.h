@@ -37,6 +37,7 @@ struct NfaArgs {
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;
   KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
+  uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)
   uint32_t* n_capacity_err;  // keys that hit CEP_KEY_CAPACITY
 };
 

@@ -93,6 +93,24 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
   return hipGetLastError();
 }
 
+// keys by estimated work, longest first (the NFA's lane order, session.cpp)
+hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
+                             uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
+  hipLaunchKernelGGL(iota_u32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, iota_tmp, n);
+  size_t need = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, need, est, est_sorted, iota_tmp, order, (int)n,
+                                                              0, 32, st);
+  if (e != hipSuccess) return e;
+  if (need > tmp_bytes) {
+    if (tmp) (void)hipFree(tmp);
+    tmp = nullptr;
+    tmp_bytes = 0;
+    if ((e = hipMalloc(&tmp, need)) != hipSuccess) return e;
+    tmp_bytes = need;
+  }
+  return hipcub::DeviceRadixSort::SortPairsDescending(tmp, need, est, est_sorted, iota_tmp, order, (int)n, 0, 32, st);
+}
+
 // ---- synthetic arrival order: CSR position p of key k, index j -> sort key j * n_keys + k
 __global__ void __launch_bounds__(256) arrival_keys(const uint64_t* __restrict__ key_off, uint64_t n_keys,
                                                     uint64_t* skey, uint32_t* kid) {

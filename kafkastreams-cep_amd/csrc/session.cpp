@@ -90,9 +90,14 @@ struct QueryRt {
   DBuf d_q, d_code;
   hipModule_t mod = nullptr;  // JIT tier: the query's own nfa kernel (cep_nfa_jit)
   hipFunction_t fn = nullptr;
+  hipFunction_t fn_est = nullptr;  // cep_nfa_est (queries whose begin stage has one BEGIN edge)
   double jit_compile_s = 0;
+  DBuf est, order, order_tmp, est_sorted;
+  void* sort_tmp = nullptr;  // hipCUB scratch of the lane-order sort
+  size_t sort_tmp_bytes = 0;
   ~QueryRt() {
     if (mod) (void)hipModuleUnload(mod);
+    if (sort_tmp) (void)hipFree(sort_tmp);
   }
   // results of the last batch (device)
   DBuf m_key, m_emit, m_off, p_seq, p_stage;
@@ -336,6 +341,24 @@ void run_nfa(cep_session* s, QueryRt& r) {
   float total_ms = 0;
   r.launches = 0;
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  // Lane order: keys sorted by estimated work, longest first (cep_nfa_est), so a wave's 64
+  // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
+  // start first.  Streams keep the identity order (their run queues live at the key's slot).
+  if (r.fn_est && !streaming && nk > 64) {
+    r.est.ensure(4 * nk);
+    r.est_sorted.ensure(4 * nk);
+    r.order.ensure(4 * nk);
+    r.order_tmp.ensure(4 * nk);
+    a.est = r.est.as<uint32_t>();
+    size_t size = sizeof(NfaArgs);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    HIPCHECK(hipModuleLaunchKernel(r.fn_est, (uint32_t)((nk + 3) / 4), 1, 1, 256, 1, 1, 0, s->stream, nullptr,
+                                   cfg));  // a wave per key
+    HIPCHECK(sort_keys_by_work(r.est.as<uint32_t>(), r.est_sorted.as<uint32_t>(), r.order_tmp.as<uint32_t>(),
+                               r.order.as<uint32_t>(), nk, r.sort_tmp, r.sort_tmp_bytes, s->stream));
+    a.key_list = r.order.as<uint32_t>();
+    a.n_list = (uint32_t)nk;
+  }
   HIPCHECK(launch_nfa_tier(r, a, nk, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   r.launches++;
@@ -531,6 +554,8 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         std::vector<char> co = jit_code_object(queries[i]->jitSource, &r->jit_compile_s);
         HIPCHECK(hipModuleLoadData(&r->mod, co.data()));
         HIPCHECK(hipModuleGetFunction(&r->fn, r->mod, "cep_nfa_jit"));
+        if (queries[i]->jitSource.find("cep_nfa_est") != std::string::npos)  // (a failed lookup would stick)
+          HIPCHECK(hipModuleGetFunction(&r->fn_est, r->mod, "cep_nfa_est"));
       }
       s->qs.push_back(std::move(r));
     }

@@ -40,7 +40,6 @@ def queries():
     qs = {k: W.stock_query("readme", **kw).to_ir() for k, kw in VARIANTS.items()}
     qs["test_nodip"] = _test_variant(lambda k, v, ts, s: v.price > s.get("avg")).to_ir()
     qs["test_notake"] = _test_variant(lambda k, v, ts, s: v.price > s.get("avg") + 1000000).to_ir()
-    qs["test_takeall"] = _test_variant(lambda k, v, ts, s: v.price > s.get("avg") - 1000000).to_ir()
     return qs
 
 
