@@ -61,8 +61,14 @@ namespace cep {
 
 constexpr uint32_t kNoSk = 0xFF;
 constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at the current event
-constexpr uint32_t kQuietChunk = 16;        // events a runs-free lane scans per driver step
-constexpr uint32_t kWalkFlush = 8;          // a queue this long drains the wave's walk queues
+#ifndef CEP_QUIET_CHUNK
+#define CEP_QUIET_CHUNK 16
+#endif
+#ifndef CEP_WALK_FLUSH
+#define CEP_WALK_FLUSH 24
+#endif
+constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
+constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
 

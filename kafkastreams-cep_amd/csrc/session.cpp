@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -270,7 +271,10 @@ void run_nfa(cep_session* s, QueryRt& r) {
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   s->rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
-  const uint32_t wcap = 32;  // deferred walks per key between drains (nfa_lane.h)
+  // deferred walks a key can queue (nfa_lane.h drains at CEP_WALK_FLUSH; $CEP_WALK_CAP: tuning)
+  uint32_t wcap = 64;
+  if (const char* e = std::getenv("CEP_WALK_CAP"))
+    if (std::atoi(e) > 0) wcap = (uint32_t)std::atoi(e);
   s->walks.ensure(walkq_size(std::max<uint64_t>(nk, 1), wcap));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 

@@ -98,12 +98,12 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       rings_batch.resize(ring_bytes(8, nslots, rc) / 16 + 64);
       scribble(rings_batch.data(), rings_batch.size() * 16);
     }
-    std::vector<v4u> walks(walkq_bytes(nslots, 32) / 16 + 64);
+    std::vector<v4u> walks(walkq_bytes(nslots, 64) / 16 + 64);
     scribble(walks.data(), walks.size() * 16);
     a.rings = streaming ? g_stream.rings.data() : rings_batch.data();
     a.rcap = rc;
     a.walks = walks.data();
-    a.wcap = 32;
+    a.wcap = 64;
     a.defer = (uint32_t)df;
     blockDim.x = 256;
     for (uint64_t s = 0; s < nslots; s++) {

@@ -38,3 +38,8 @@ inline double __dadd_rn(double a, double b) { return a + b; }
 inline double __dsub_rn(double a, double b) { return a - b; }
 inline double __dmul_rn(double a, double b) { return a * b; }
 inline double __ddiv_rn(double a, double b) { return a / b; }
+// a wave of one lane: there is no lane below/above to read from
+template <class T>
+inline T __shfl_down(T, int, int = 64) {
+  return T(0);
+}
