@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
     xn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + wbase + (uint64_t)lane * 4));
     if (NCOL > 1) yn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + wbase + (uint64_t)lane * 4));
   }
-#pragma unroll 1
+#pragma unroll 2
   for (int q = 0; q < kStSteps; q++) {
     {
       const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
@@ -316,8 +316,11 @@ __device__ __forceinline__ uint64_t spread4(uint32_t x16) {
 // from the group and tile counts, a block scan for the threads' offsets and key ranks.
 template <int M>
 __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
+  // a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
+  constexpr uint32_t kStage = 2048;
   __shared__ uint32_t s_wsum[kStThreads / 64];
   __shared__ uint64_t s_toff[kStThreads / 64];
+  __shared__ uint2 s_stage[kStage];  // (key, sequence number of the final event)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t t = blockIdx.x;
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
@@ -360,7 +363,10 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const uint32_t excl = woff + incl - packed;
   const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
   if (t + 1 == gridDim.x && tid == kStThreads - 1) *A.total = toff + ((woff + incl) >> 16);  // all matches
+  const uint32_t tile_total = (s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3]) >> 16;
+  const bool staged = tile_total <= kStage;  // block-uniform
   uint64_t o = toff + (excl >> 16);
+  uint32_t so = excl >> 16;  // slot within the tile
   const uint32_t rank0 = A.tile_rank[t] + (excl & 0xFFFF);
   uint32_t cur_rank = 0xFFFFFFFFu, key = 0;
   uint64_t kstart = 0;
@@ -377,7 +383,9 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
       kstart = A.key_off[key];
     }
     const uint32_t seq = (uint32_t)(p - kstart);
-    if (o < A.out_cap) {
+    if (staged) {
+      s_stage[so++] = uint2{key, seq};
+    } else if (o < A.out_cap) {
       A.m_key[o] = key;
 #pragma unroll
       for (int x = 0; x < M; x++) A.p_seq[o * M + x] = seq - x;
@@ -385,6 +393,24 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
       atomicOr(A.overflow, 1u);
     }
     o++;
+  }
+  if (!staged) return;
+  __syncthreads();
+  // thread i writes matches i, i + 256, ...: adjacent threads, adjacent slots
+  for (uint32_t i = tid; i < tile_total; i += kStThreads) {
+    const uint64_t slot = toff + i;
+    const uint2 e = s_stage[i];
+    if (slot < A.out_cap) {
+      A.m_key[slot] = e.x;
+      if (M == 3) {  // one 12-B store per match
+        *reinterpret_cast<uint3*>(A.p_seq + slot * 3) = uint3{e.y, e.y - 1, e.y - 2};
+      } else {
+#pragma unroll
+        for (int x = 0; x < M; x++) A.p_seq[slot * M + x] = e.y - x;
+      }
+    } else {
+      atomicOr(A.overflow, 1u);
+    }
   }
 }
 
