@@ -4,7 +4,8 @@
 // (CEPProcessor.process, CEPProcessor.java:155-163) and each key's NFA sees that key's records
 // in that order.  A batch handed over in arrival order (one key id per event) is
 // partitioned on the device: a stable LSD radix sort of (key, arrival index) pairs by key
-// (rocPRIM through hipCUB), key counts -> key_off (exclusive scan), then one gather per column.
+// (rocPRIM through hipCUB), key_off by a binary search per key over the sorted keys, then one
+// gather per column.
 // Stability is what keeps every key's events in arrival order.  All passes are HBM-bound.
 //
 // Also the synthetic arrival-order stream of the bench/tests: the CSR stream of
@@ -22,17 +23,25 @@ __global__ void __launch_bounds__(256) iota_u32(uint32_t* v, uint64_t n) {
   if (i < n) v[i] = (uint32_t)i;
 }
 
-// counts per key (atomics; the order of the adds does not matter) and a range check
-__global__ void __launch_bounds__(256) count_keys(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_keys,
-                                                  unsigned long long* cnt, unsigned* bad) {
+// range check of the key ids (the sort only looks at the bits of n_keys - 1)
+__global__ void __launch_bounds__(256) check_keys(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_keys,
+                                                  unsigned* bad) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = key[i];
-  if (k >= n_keys) {
-    atomicOr(bad, 1u);
-    return;
+  if (i < n && key[i] >= n_keys) atomicOr(bad, 1u);
+}
+
+// key_off[k] = first position of a key >= k in the sorted keys (binary search per key)
+__global__ void __launch_bounds__(256) key_offsets(const uint32_t* __restrict__ sorted, uint64_t n, uint64_t n_keys,
+                                                   uint64_t* key_off) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k > n_keys) return;
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (sorted[mid] < k) lo = mid + 1;
+    else hi = mid;
   }
-  atomicAdd(cnt + k, 1ull);
+  key_off[k] = lo;
 }
 
 // CSR position p <- arrival index perm[p], for every column (4- or 8-byte values) and ts
@@ -59,13 +68,11 @@ static int key_bits(uint64_t n_keys) {
 
 // Device scratch of partition(): bytes needed for n events over n_keys keys.
 size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys) {
+  (void)n_keys;
   size_t tmp = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1));
-  size_t scan = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                   (int)(n_keys + 1));
-  return std::max(tmp, scan) + 256;
+  return tmp + 256;
 }
 
 // arrival-order batch -> key_off[n_keys + 1], perm[n] (arrival index of each CSR position),
@@ -74,22 +81,19 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
                      hipStream_t st) {
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (n_keys + 1), st);
-  if (e != hipSuccess) return e;
+  (void)cnt;
   const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  hipError_t e = hipSuccess;
   if (n) {
+    hipLaunchKernelGGL(check_keys, dim3(blocks), dim3(256), 0, st, key, n, n_keys, bad);
     hipLaunchKernelGGL(iota_u32, dim3(blocks), dim3(256), 0, st, idx, n);
-    hipLaunchKernelGGL(count_keys, dim3(blocks), dim3(256), 0, st, key, n, n_keys, (unsigned long long*)cnt, bad);
+    size_t tmp = scratch_bytes;
+    e = hipcub::DeviceRadixSort::SortPairs(scratch, tmp, key, sorted_keys, idx, perm, (int)n, 0, key_bits(n_keys), st);
+    if (e != hipSuccess) return e;
   }
-  size_t tmp = scratch_bytes;
-  e = hipcub::DeviceScan::ExclusiveSum(scratch, tmp, (unsigned long long*)cnt, (unsigned long long*)key_off,
-                                       (int)(n_keys + 1), st);
-  if (e != hipSuccess || n == 0) return e;
-  if (e != hipSuccess) return e;
-  tmp = scratch_bytes;
-  e = hipcub::DeviceRadixSort::SortPairs(scratch, tmp, key, sorted_keys, idx, perm, (int)n, 0, key_bits(n_keys), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(gather_cols, dim3(blocks), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in, ts_out);
+  hipLaunchKernelGGL(key_offsets, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, st, sorted_keys, n, n_keys,
+                     key_off);
+  if (n) hipLaunchKernelGGL(gather_cols, dim3(blocks), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in, ts_out);
   return hipGetLastError();
 }
 
