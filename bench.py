@@ -14,7 +14,7 @@ all-gathers counts/checksums and reduces the watermark.
 Prints ONE JSON line on rank 0 (contract in the task statement; fields documented in
 DESIGN.md §7).  `roofline` prices cep_nfa_jit at SURVEY §8(d)'s algorithmic bytes (columns read
 once + 4 B per emitted event id + 4 B per match) against 8 TB/s; `cpu_baseline` times the
-oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/64 key
+oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/8 key
 sample on this host's cores.
 """
 import argparse
@@ -160,10 +160,36 @@ def secondary_strict(device, steps, warmup, dist):
            "ms_per_step": 1e3 * el / steps,
            "roofline": {"bound": "hbm", "achieved": alg / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": load_traffic("stencil"), "kernel": "stencil_mask+stencil_scan+stencil_emit",
+                        "traffic": load_traffic("stencil"), "kernel": "stencil_mask+stencil_emit",
                         "kernel_ms": kms, "algorithmic_bytes": alg}}
     s.close()
     return res
+
+
+def other_configs(device, steps, warmup, dist, keys):
+    """BASELINE configs 4 and 5 on the cfg-3 stream at `keys` keys x ~1000 events on one GPU
+    (parity-tested at reduced size in tests/test_gpu_parity.py): cfg 4 = skip_till_any Kleene+
+    with folds and a 10 ms window, cfg 5 = 64 stock-query variants in one session, which
+    reads the stream once per query launch.  Reported as stream events/s and, for cfg 5,
+    query-events/s (stream events x queries)."""
+    cfg = W.CONFIGS[3]
+    stream = N.synth_stream("stock", cfg.seed, keys, 1000, 0, device)
+    out = {}
+    for name, queries in (("cfg4", [W.any_kleene_query()]), ("cfg5", W.multi_queries(64))):
+        qs = [N.Query(p.to_ir()) for p in queries]
+        s = N.Session(qs, device=device)
+        el, _, _ = run_steps(s, stream, steps, warmup, dist)
+        kms = [s.timing(i)[0] for i in range(len(qs))]
+        n_m = sum(s.digest(i)[0] for i in range(len(qs)))
+        s.close()
+        ev_s = stream.n_events * steps / el
+        out[name] = {"workload": ("cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms" if name == "cfg4"
+                                  else "cfg5: 64 stock-query variants, one session") +
+                     f", {keys} keys x ~1000 events ({stream.n_events} events) on 1 GPU",
+                     "value": ev_s, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
+                     "queries": len(qs), "query_events_per_s": ev_s * len(qs),
+                     "kernel_ms_sum": float(sum(kms)), "matches_per_step": int(n_m)}
+    return out
 
 
 def end_to_end(args, device, dist):
@@ -209,10 +235,12 @@ def main():
     ap.add_argument("--mean", type=int, default=1000, help="mean events per key")
     ap.add_argument("--variant", default="readme", choices=["readme", "test"])
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
-    ap.add_argument("--cpu-every", type=int, default=64)
+    ap.add_argument("--cpu-every", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the arrival-order end-to-end figure")
+    ap.add_argument("--no-other", action="store_true", help="skip the cfg 4 / cfg 5 figures")
+    ap.add_argument("--other-keys", type=int, default=100_000, help="keys of the cfg 4 / cfg 5 figures")
     args = ap.parse_args()
 
     dist = Dist()
@@ -274,6 +302,8 @@ def main():
         if dist.world == 1 and not args.no_e2e:
             sess.close()
             out["end_to_end"] = end_to_end(args, device, dist)
+        if dist.world == 1 and not args.no_other:
+            out["other_configs"] = other_configs(device, max(1, args.steps // 2), 1, dist, args.other_keys)
         print(json.dumps(out), flush=True)
     sess.close()
     dist.close()

@@ -209,6 +209,19 @@ int cep_watermark(cep_session* s, int64_t* out);
  * stream (ms): the matching kernel launches (kernel_ms, `launches` of them: the NFA kernel
  * incl. capacity retries, or stencil_mask + stencil_emit) and the
  * setup/compaction kernels (aux_ms). */
+/* ---- streaming-session snapshot / restore ----
+ * The reference's persistent mode stores the NFA's run queue and buffer nodes after every
+ * record (CEPProcessor.java:121-131,159-160; nfa/ComputationStageSerDe.java:53-125;
+ * nfa/buffer/impl/TimedKeyValueSerDes.java:42-63) and reloads them in init().  Here the
+ * complete per-key NFA state of a streaming session (cep_opts.streaming = 1) is one
+ * versioned blob.  cep_session_snapshot(s, NULL, 0, &size) returns the size; with a buffer
+ * of at least that size it writes the blob (the session is unchanged).  cep_session_restore
+ * loads a blob into a streaming session created over the same queries and max_runs; the
+ * next cep_push_batch continues every key's stream where the snapshot left it.  Blobs from
+ * other queries, options or versions are rejected with CEP_E_INVALID before any change. */
+int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size);
+int cep_session_restore(cep_session* s, const void* buf, size_t size);
+
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);
 
 const char* cep_last_error(void);

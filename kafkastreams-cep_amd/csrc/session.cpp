@@ -82,6 +82,8 @@ struct StreamState {
   DBuf rings, nodes, preds, carry, tops;  // tops: {node_top, pred_top} (device)
   uint64_t n_keys = 0, node_cap = 0, pred_cap = 0;
   uint32_t node_used = 0, pred_used = 0;  // pool tops after the last batch
+  uint32_t rcap = 0;                      // run-queue slots per key (ring layout)
+  uint64_t ring_bytes = 0;
   bool init = false;
 };
 
@@ -289,6 +291,8 @@ void run_nfa(cep_session* s, QueryRt& r) {
       S.tops.ensure(2 * sizeof(uint32_t));
       HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
       S.rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
+      S.rcap = rcap;
+      S.ring_bytes = ring_size(r.F, std::max<uint64_t>(nk, 1), rcap);
       S.init = true;
     } else if (nk != S.n_keys) {
       throw std::invalid_argument("the batches of a streaming session share one key space (n_keys)");
@@ -835,6 +839,157 @@ int cep_watermark(cep_session* s, int64_t* out) {
   if (!s || !out) return fail(CEP_E_INVALID, "null argument");
   *out = s->watermark;
   return CEP_OK;
+}
+
+// ---- streaming-session snapshot / restore ----
+// Stands for the reference's persistent mode: CEPProcessor keeps the NFA's run queue in a
+// store, serialised with Kryo after every record (CEPProcessor.java:121-131,159-160;
+// nfa/ComputationStageSerDe.java:53-125) and the buffer nodes in their own store
+// (nfa/buffer/impl/TimedKeyValueSerDes.java:42-63).  Here the whole per-key state of every
+// query of a streaming session - KeyCarry per key, the run-queue rings, the used prefix of the
+// node/predecessor pools and the pool tops - is one versioned little-endian blob.  Restoring
+// it into a fresh streaming session over the same queries and options continues every key's
+// stream exactly (tests/test_gpu_parity.py::test_streaming_snapshot_restore).
+namespace {
+constexpr uint64_t kSnapMagic = 0x31504E5350454300ull;  // "\0CEPSNP1"
+constexpr uint32_t kSnapVersion = 1;
+
+uint64_t query_fingerprint(const cep_query* q) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  mix(q->code.data(), q->code.size() * sizeof(uint32_t));
+  mix(q->jitSource.data(), q->jitSource.size());
+  mix(&q->info.kind, sizeof q->info.kind);
+  return h;
+}
+
+struct SnapQueryHdr {
+  uint64_t fingerprint, n_keys, ring_bytes;
+  uint32_t F, rcap, node_used, pred_used, init, pad;
+};
+
+uint64_t snap_size(const cep_session* s) {
+  uint64_t n = 32;  // magic, version, n_queries, watermark, reserved
+  for (auto& r : s->qs) {
+    n += sizeof(SnapQueryHdr);
+    const StreamState& S = r->st;
+    if (S.init)
+      n += sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1) + S.ring_bytes + sizeof(Node) * S.node_used +
+           sizeof(Pred) * S.pred_used;
+  }
+  return n;
+}
+}  // namespace
+
+int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size) {
+  if (!s || !size) return fail(CEP_E_INVALID, "null argument");
+  if (!s->opts.streaming) return fail(CEP_E_STATE, "snapshot needs a streaming session (cep_opts.streaming)");
+  const uint64_t need = snap_size(s);
+  *size = (size_t)need;
+  if (!buf) return CEP_OK;  // size query
+  if (cap < need) return fail(CEP_E_INVALID, "snapshot buffer too small (see *size)");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    uint8_t* o = static_cast<uint8_t*>(buf);
+    const uint32_t nq = (uint32_t)s->qs.size();
+    std::memset(o, 0, 32);
+    std::memcpy(o, &kSnapMagic, 8);
+    std::memcpy(o + 8, &kSnapVersion, 4);
+    std::memcpy(o + 12, &nq, 4);
+    std::memcpy(o + 16, &s->watermark, 8);
+    o += 32;
+    for (auto& r : s->qs) {
+      const StreamState& S = r->st;
+      SnapQueryHdr h{query_fingerprint(r->q), S.n_keys, S.ring_bytes, (uint32_t)r->F, S.rcap,
+                     S.node_used, S.pred_used, S.init ? 1u : 0u, 0};
+      std::memcpy(o, &h, sizeof h);
+      o += sizeof h;
+      if (!S.init) continue;
+      auto d2h = [&](const void* src, uint64_t n) {
+        if (n) HIPCHECK(hipMemcpy(o, src, n, hipMemcpyDeviceToHost));
+        o += n;
+      };
+      d2h(S.carry.p, sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1));
+      d2h(S.rings.p, S.ring_bytes);
+      d2h(S.nodes.p, sizeof(Node) * S.node_used);
+      d2h(S.preds.p, sizeof(Pred) * S.pred_used);
+    }
+  });
+}
+
+int cep_session_restore(cep_session* s, const void* buf, size_t size) {
+  if (!s || !buf) return fail(CEP_E_INVALID, "null argument");
+  if (!s->opts.streaming) return fail(CEP_E_STATE, "restore needs a streaming session (cep_opts.streaming)");
+  const uint8_t* p = static_cast<const uint8_t*>(buf);
+  const uint8_t* end = p + size;
+  uint64_t magic = 0;
+  uint32_t ver = 0, nq = 0;
+  if (size < 32) return fail(CEP_E_INVALID, "snapshot truncated");
+  std::memcpy(&magic, p, 8);
+  std::memcpy(&ver, p + 8, 4);
+  std::memcpy(&nq, p + 12, 4);
+  if (magic != kSnapMagic) return fail(CEP_E_INVALID, "not a cep snapshot");
+  if (ver != kSnapVersion) return fail(CEP_E_INVALID, "unsupported snapshot version");
+  if (nq != s->qs.size()) return fail(CEP_E_INVALID, "snapshot holds a different number of queries");
+  int64_t wm = 0;
+  std::memcpy(&wm, p + 16, 8);
+  // validate everything before touching the session
+  {
+    const uint8_t* q = p + 32;
+    for (auto& r : s->qs) {
+      SnapQueryHdr h;
+      if (q + sizeof h > end) return fail(CEP_E_INVALID, "snapshot truncated");
+      std::memcpy(&h, q, sizeof h);
+      q += sizeof h;
+      if (h.fingerprint != query_fingerprint(r->q)) return fail(CEP_E_INVALID, "snapshot of a different query");
+      if (!h.init) continue;
+      const uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
+      if (h.rcap != rcap || h.F != (uint32_t)r->F || h.ring_bytes != ring_size(r->F, std::max<uint64_t>(h.n_keys, 1), rcap))
+        return fail(CEP_E_INVALID, "snapshot taken with other session options (max_runs)");
+      const uint64_t n = sizeof(KeyCarry) * std::max<uint64_t>(h.n_keys, 1) + h.ring_bytes +
+                         sizeof(Node) * (uint64_t)h.node_used + sizeof(Pred) * (uint64_t)h.pred_used;
+      if ((uint64_t)(end - q) < n) return fail(CEP_E_INVALID, "snapshot truncated");
+      q += n;
+    }
+  }
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    const uint8_t* q = p + 32;
+    for (auto& r : s->qs) {
+      SnapQueryHdr h;
+      std::memcpy(&h, q, sizeof h);
+      q += sizeof h;
+      StreamState& S = r->st;
+      S.init = false;
+      if (!h.init) continue;
+      auto h2d = [&](DBuf& dst, uint64_t n) {
+        dst.ensure(std::max<uint64_t>(n, 16));
+        if (n) HIPCHECK(hipMemcpy(dst.p, q, n, hipMemcpyHostToDevice));
+        q += n;
+      };
+      S.n_keys = h.n_keys;
+      S.rcap = h.rcap;
+      S.ring_bytes = h.ring_bytes;
+      h2d(S.carry, sizeof(KeyCarry) * std::max<uint64_t>(h.n_keys, 1));
+      h2d(S.rings, h.ring_bytes);
+      S.node_cap = std::max<uint64_t>(h.node_used, 1);
+      S.pred_cap = std::max<uint64_t>(h.pred_used, 1);
+      h2d(S.nodes, sizeof(Node) * (uint64_t)h.node_used);
+      h2d(S.preds, sizeof(Pred) * (uint64_t)h.pred_used);
+      S.node_used = h.node_used;
+      S.pred_used = h.pred_used;
+      const uint32_t tops[2] = {h.node_used, h.pred_used};
+      S.tops.ensure(2 * sizeof(uint32_t));
+      HIPCHECK(hipMemcpy(S.tops.p, tops, sizeof tops, hipMemcpyHostToDevice));
+      S.init = true;
+    }
+    s->watermark = wm;
+  });
 }
 
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches) {

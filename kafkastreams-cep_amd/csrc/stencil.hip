@@ -22,6 +22,9 @@
 // through each other).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <type_traits>
+
 #include "cep_layout.h"
 #include "nfa_device.h"
 #include "stencil_args.h"
@@ -111,10 +114,13 @@ __device__ __forceinline__ bool in_range(int64_t v, int64_t lo, int64_t hi) { re
 // the previous step (wave-uniform carries).  Key starts come the same way from the bitmap.
 constexpr int kStWave = kStTile / (kStThreads / 64);  // 4096 events per wave
 constexpr int kStSteps = kStWave / 256;               // 16 load steps per wave
+constexpr int kStDefaultPF = 1;
 
 template <int M, bool RANGE, int NCOL>
 struct StEval {
   int32_t lo[M][2], hi[M][2];
+  uint32_t span[M][2];
+  bool never = false;  // an empty range: no stage-s event, no match (the slow path handles it)
   __device__ __forceinline__ explicit StEval(const StencilArgs& A) {
     if (RANGE) {
       // int32 bounds (a range outside int32 is clamped: empty stays empty)
@@ -129,6 +135,10 @@ struct StEval {
             lo[s][c] = 1;
             hi[s][c] = 0;
           }
+          // lo <= x <= hi  <=>  (uint)(x - lo) <= (uint)(hi - lo): one subtract and one
+          // compare, both vector ops (no scalar AND of two compare masks)
+          span[s][c] = (uint32_t)hi[s][c] - (uint32_t)lo[s][c];
+          if (c < NCOL && lo[s][c] > hi[s][c]) never = true;
         }
     }
   }
@@ -148,6 +158,25 @@ struct StEval {
     if (NCOL > 1) m &= __builtin_amdgcn_ballot_w64(x1 >= lo[s][1]) & __builtin_amdgcn_ballot_w64(x1 <= hi[s][1]);
     return m;
   }
+  // stage s over the 4 events of a step: W[k] = ballot word of event 4 l + k.  Every
+  // operation is a vector op whose result lands in scalar registers (the compare mask);
+  // the scalar unit, shared by the CU's four SIMDs, is this kernel's tightest resource.
+  __device__ __forceinline__ bool in1(int s, int c, int32_t v) const {
+    return (uint32_t)v - (uint32_t)lo[s][c] <= span[s][c];
+  }
+  __device__ __forceinline__ void ballot4(int s, const v4i x, const v4i y, uint64_t* W) const {
+    if (NCOL == 1) {
+      W[0] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.x));
+      W[1] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.y));
+      W[2] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.z));
+      W[3] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.w));
+    } else {
+      W[0] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.x)) & __builtin_amdgcn_ballot_w64(in1(s, 1, y.x));
+      W[1] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.y)) & __builtin_amdgcn_ballot_w64(in1(s, 1, y.y));
+      W[2] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.z)) & __builtin_amdgcn_ballot_w64(in1(s, 1, y.z));
+      W[3] = __builtin_amdgcn_ballot_w64(in1(s, 0, x.w)) & __builtin_amdgcn_ballot_w64(in1(s, 1, y.w));
+    }
+  }
   __device__ __forceinline__ void one(const StencilArgs& A, uint64_t p, uint32_t* P, int bit) const {
     if (p >= A.n_events) return;
     if (RANGE) {
@@ -163,8 +192,9 @@ struct StEval {
   }
 };
 
-template <int M, bool RANGE, int NCOL>
+template <int M, bool RANGE, int NCOL, int PF>
 __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
+  static_assert(kStSteps % PF == 0, "prefetch depth divides the wave's steps");
   constexpr int H = M - 1;              // events a window reaches back
   __shared__ uint32_t s_cnt[kStThreads / 64];
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
@@ -172,10 +202,39 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
   const StEval<M, RANGE, NCOL> ev(A);
+  const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never;
+  // The fast path's first PF steps are requested before anything else: the key-start words
+  // and the seed events below are dependent round trips, and a wave only lives 16 steps.
+  const v4i* c0 = reinterpret_cast<const v4i*>(A.col[0] + wbase) + lane;
+  const v4i* c1 = reinterpret_cast<const v4i*>(A.col[NCOL - 1] + wbase) + lane;
+  v4i xb[PF], yb[PF];
+#pragma unroll
+  for (int d = 0; d < PF; d++) xb[d] = yb[d] = v4i{0, 0, 0, 0};
+  if (fast) {
+#pragma unroll
+    for (int d = 0; d < PF; d++) {
+      xb[d] = __builtin_nontemporal_load(c0 + d * 64);
+      yb[d] = NCOL > 1 ? __builtin_nontemporal_load(c1 + d * 64) : xb[d];
+    }
+  }
   // the wave's 64 key-start words, one per lane (word w: events 64 w .. 64 w + 63)
-  uint64_t bw = 0;
-  if (H > 0 && wbase + (uint64_t)lane * 64 < A.n_events) bw = A.bnd[wbase / 64 + lane];
-  const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events;
+  // (all of the wave's start-up loads are unconditional, clamped in bounds and issued
+  // together: one memory round trip before the first step, not three)
+  const uint64_t last_word = (A.n_events - 1) / 64;  // n_events >= 1: the tile exists
+  const uint64_t bwi = wbase / 64 + lane;
+  const uint64_t bwl = H > 0 ? A.bnd[bwi < last_word ? bwi : last_word] : 0;
+  // the 8 events before the wave (lanes 0..7; the others load the same lines)
+  const uint64_t sp0 = (wbase >= 8 ? wbase - 8 : 0) + (uint64_t)(lane & 7);
+  const uint64_t sp = sp0 < A.n_events ? sp0 : A.n_events - 1;
+  int32_t sx0 = 0, sx1 = 0;
+  if (RANGE && H > 0) {
+    sx0 = A.col[0][sp];
+    sx1 = A.col[NCOL - 1][sp];
+  }
+  // the key-start word before the wave (wbase % 64 == 0)
+  const uint64_t bprev = H > 0 ? A.bnd[wbase >= 64 ? wbase / 64 - 1 : 0] : 0;
+  if (RANGE && H > 0) asm volatile("" ::"v"(sx0), "v"(sx1));  // keeps the seed loads up here
+  const uint64_t bw = (wbase + (uint64_t)lane * 64 < A.n_events) ? bwl : 0;
   // steps with a key start (bit 4q + x: word x of step q is non-zero), mostly none
   const uint64_t kstep = H > 0 ? __ballot(bw != 0) : 0;
   // Ballot words of the previous step: bit l of W[s][k] = stage s holds at event 4l + k.
@@ -186,69 +245,74 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
     uint32_t P[M];
 #pragma unroll
     for (int s = 0; s < M; s++) P[s] = 0;
-    if (H > 0 && lane < 8 && wbase >= (uint64_t)(8 - lane)) ev.one(A, wbase - 8 + lane, P, 0);
+    if (H > 0 && lane < 8 && wbase >= (uint64_t)(8 - lane)) {
+      if (RANGE && sp0 < A.n_events) ev.range(sx0, sx1, P, 0);
+      else if (!RANGE) ev.one(A, wbase - 8 + lane, P, 0);
+    }
 #pragma unroll
     for (int s = 0; s < M; s++) {
       const uint64_t b = __ballot(P[s] & 1u);  // bit x: event wbase - 8 + x
 #pragma unroll
       for (int k = 0; k < 4; k++) pW[s][k] = (((b >> k) & 1ull) << 62) | (((b >> (4 + k)) & 1ull) << 63);
     }
-    const uint64_t w = (H > 0 && wbase >= 8) ? A.bnd[wbase / 64 - 1] : 0;  // wbase % 64 == 0
+    const uint64_t w = (H > 0 && wbase >= 8) ? bprev : 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) pK[k] = (((w >> (56 + k)) & 1ull) << 62) | (((w >> (60 + k)) & 1ull) << 63);
   }
-  uint32_t cnt = 0;
+  bool pk_any = ((pK[0] | pK[1] | pK[2] | pK[3]) >> 62) != 0;
   uint64_t myword = 0;  // mask word wbase / 64 + lane = word k of step q for lane 4q + k
-  // one step per iteration, the next step's load in flight (occupancy supplies the rest of
-  // the memory parallelism; the step body is scalar-heavy and must not be unrolled 16x)
-  v4i xn = {0, 0, 0, 0}, yn = {0, 0, 0, 0};
-  if (fast) {
-    xn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + wbase + (uint64_t)lane * 4));
-    if (NCOL > 1) yn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + wbase + (uint64_t)lane * 4));
-  }
-#pragma unroll 2
-  for (int q = 0; q < kStSteps; q++) {
-    {
-      const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
-      const v4i x = xn, y = NCOL > 1 ? yn : xn;
-      if (fast && q + 1 < kStSteps) {
-        xn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0 + 256));
-        if (NCOL > 1) yn = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0 + 256));
+  // step q of the wave: x/y hold its 4 events per lane on the fast path (FAST: a
+  // std::integral_constant, so each loop below gets its own straight-line body)
+  auto step = [&](const int q, const v4i x, const v4i y, auto fast_c) {
+    constexpr bool FAST = decltype(fast_c)::value;
+    const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
+    // stage words of this step (wave-uniform, scalar registers): bit l of W[s][k] = stage s
+    // holds at event 4l + k
+    uint64_t W[M][4];
+    if (FAST) {
+#pragma unroll
+      for (int s = 0; s < M; s++) ev.ballot4(s, x, y, W[s]);
+    } else {
+      uint32_t P[M];
+#pragma unroll
+      for (int s = 0; s < M; s++) P[s] = 0;
+      if (RANGE && A.aligned && e0 + 4 <= A.n_events) {
+        const v4i xs = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0));
+        v4i ys = xs;
+        if (NCOL > 1) ys = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0));
+        ev.range(xs.x, ys.x, P, 0);
+        ev.range(xs.y, ys.y, P, 1);
+        ev.range(xs.z, ys.z, P, 2);
+        ev.range(xs.w, ys.w, P, 3);
+      } else if (e0 < A.n_events) {  // events past the end stay 0: no window can end there
+#pragma unroll
+        for (int i = 0; i < 4; i++) ev.one(A, e0 + i, P, i);
       }
-      // stage words of this step (wave-uniform, scalar registers): bit l of W[s][k] = stage s
-      // holds at event 4l + k
-      uint64_t W[M][4];
-      if (fast) {
 #pragma unroll
-        for (int s = 0; s < M; s++) {
-          W[s][0] = ev.ballot(s, x.x, y.x);
-          W[s][1] = ev.ballot(s, x.y, y.y);
-          W[s][2] = ev.ballot(s, x.z, y.z);
-          W[s][3] = ev.ballot(s, x.w, y.w);
-        }
-      } else {
-        uint32_t P[M];
+      for (int s = 0; s < M; s++)
 #pragma unroll
-        for (int s = 0; s < M; s++) P[s] = 0;
-        if (RANGE && A.aligned && e0 + 4 <= A.n_events) {
-          const v4i xs = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[0] + e0));
-          v4i ys = xs;
-          if (NCOL > 1) ys = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(A.col[1] + e0));
-          ev.range(xs.x, ys.x, P, 0);
-          ev.range(xs.y, ys.y, P, 1);
-          ev.range(xs.z, ys.z, P, 2);
-          ev.range(xs.w, ys.w, P, 3);
-        } else if (e0 < A.n_events) {  // events past the end stay 0: no window can end there
+        for (int k = 0; k < 4; k++) W[s][k] = __builtin_amdgcn_ballot_w64((P[s] >> k) & 1u);
+    }
+    // word k: windows ending at events 4l + k.  Stage s sits o = M-1-s events back: event
+    // 4l + k - o is word (k - o) mod 4, `cr` lanes back (bits shifted up, the previous
+    // step's top bits carried in).
+    uint64_t m[4];
 #pragma unroll
-          for (int i = 0; i < 4; i++) ev.one(A, e0 + i, P, i);
-        }
+    for (int k = 0; k < 4; k++) {
+      m[k] = ~0ull;
 #pragma unroll
-        for (int s = 0; s < M; s++)
-#pragma unroll
-          for (int k = 0; k < 4; k++) W[s][k] = __builtin_amdgcn_ballot_w64((P[s] >> k) & 1u);
+      for (int s = 0; s < M; s++) {
+        const int t = k - (M - 1 - s);
+        const int cr = t >= 0 ? 0 : (3 - t) / 4;
+        const int kk = t + 4 * cr;
+        m[k] &= cr == 0 ? W[s][kk] : ((W[s][kk] << cr) | (pW[s][kk] >> (64 - cr)));
       }
+    }
+    // A key start at any of the window's last M-1 events (offsets 0 .. M-2) kills it: only
+    // in steps holding a key start or right after one (a wave-uniform branch, rarely taken)
+    if (H > 0 && (((kstep >> (4 * q)) & 0xF) || pk_any)) {
       uint64_t K[4] = {0, 0, 0, 0};
-      if (H > 0 && ((kstep >> (4 * q)) & 0xF)) {
+      if ((kstep >> (4 * q)) & 0xF) {
         // this lane's 4 key-start bits: word 4q + lane/16 of the wave (lanes 4q..4q+3 hold
         // them), nibble lane % 16
         const uint64_t b0 = __shfl(bw, 4 * q, 64), b1 = __shfl(bw, 4 * q + 1, 64);
@@ -259,40 +323,61 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
 #pragma unroll
         for (int k = 0; k < 4; k++) K[k] = __builtin_amdgcn_ballot_w64((B >> k) & 1u);
       }
-      // word k: windows ending at events 4l + k.  Stage s sits o = M-1-s events back: event
-      // 4l + k - o is word (k - o) mod 4, `cr` lanes back (bits shifted up, the previous
-      // step's top bits carried in).  A key start at any of the window's last M-1 events
-      // (offsets 0 .. M-2) kills it.
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint64_t m = ~0ull;
-#pragma unroll
-        for (int s = 0; s < M; s++) {
-          const int t = k - (M - 1 - s);
-          const int cr = t >= 0 ? 0 : (3 - t) / 4;
-          const int kk = t + 4 * cr;
-          m &= cr == 0 ? W[s][kk] : ((W[s][kk] << cr) | (pW[s][kk] >> (64 - cr)));
-        }
+      for (int k = 0; k < 4; k++)
 #pragma unroll
         for (int o = 0; o < H; o++) {
           const int t = k - o;
           const int cr = t >= 0 ? 0 : (3 - t) / 4;
           const int kk = t + 4 * cr;
-          m &= ~(cr == 0 ? K[kk] : ((K[kk] << cr) | (pK[kk] >> (64 - cr))));
+          m[k] &= ~(cr == 0 ? K[kk] : ((K[kk] << cr) | (pK[kk] >> (64 - cr))));
         }
-        cnt += (uint32_t)__popcll(m);
-        if (lane == 4 * q + k) myword = m;
+#pragma unroll
+      for (int k = 0; k < 4; k++) pK[k] = K[k];
+      pk_any = ((K[0] | K[1] | K[2] | K[3]) >> 62) != 0;  // only the top two bits carry
+    }
+    // lane 4q + k keeps word k (vector compare + select: no scalar work)
+    const int lrel = lane - 4 * q;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (lrel == k) myword = m[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int s = 0; s < M; s++) pW[s][k] = W[s][k];
+  };
+  if (fast) {
+    // PF steps per chunk; the next chunk's PF loads are issued before this chunk's steps
+    // run.  The loads are unconditional (the last chunk re-reads itself): a load under a
+    // branch makes the waitcnt pass drain every outstanding load (vmcnt(0)) before the
+    // first use, which serialises the wave on HBM latency.
+#pragma unroll 1
+    for (int c = 0; c < kStSteps; c += PF) {
+      const int cn = c + PF < kStSteps ? c + PF : c;
+      v4i xn[PF], yn[PF];
+#pragma unroll
+      for (int d = 0; d < PF; d++) {
+        xn[d] = __builtin_nontemporal_load(c0 + (cn + d) * 64);
+        yn[d] = NCOL > 1 ? __builtin_nontemporal_load(c1 + (cn + d) * 64) : xn[d];
       }
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int d = 0; d < PF; d++) step(c + d, xb[d], yb[d], std::true_type{});
 #pragma unroll
-        for (int s = 0; s < M; s++) pW[s][k] = W[s][k];
-        pK[k] = K[k];
+      for (int d = 0; d < PF; d++) {
+        xb[d] = xn[d];
+        yb[d] = yn[d];
       }
     }
+  } else {
+    const v4i z = {0, 0, 0, 0};
+    for (int q = 0; q < kStSteps; q++) step(q, z, z, std::false_type{});
   }
   // one 512-B store: words 4q..4q+3 belong to step q (written when the step has an event)
   if (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) A.mask[wbase / 64 + lane] = myword;
+  // matches of the wave: popcount of each lane's word, summed over the wave once
+  uint32_t cnt = (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) ? (uint32_t)__popcll(myword) : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (lane == 0) s_cnt[wv] = cnt;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -324,15 +409,27 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t t = blockIdx.x;
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
-  // the step (256 events) holding this thread's 64: 16 lanes of each of its 4 ballot words
+  // Every independent load is issued before the first use (addresses clamped, no branches):
+  // the step (256 events) holding this thread's 64 - 16 lanes of each of its 4 ballot words -
+  // its key-start word, the tile's first key (rank -> key -> CSR start, scalar loads) and
+  // the counts of the tiles before it.
+  const bool valid = p0 < A.n_events;
+  const uint64_t pc = valid ? p0 : t * kStTile;  // a tile's first event always exists
+  const uint64_t* w = A.mask + (pc / 256) * 4;
+  const uint64_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const uint64_t Bw = A.bnd[pc / 64];
+  const uint32_t trank = A.tile_rank[t];
+  const uint32_t tkey = A.nz_key[trank];
+  const uint64_t tkstart = A.key_off[tkey];
   uint32_t ck[4] = {0, 0, 0, 0};
   uint64_t B = 0;
-  if (p0 < A.n_events) {
-    const uint64_t* w = A.mask + (p0 / 256) * 4;
+  if (valid) {
     const int sh = 16 * (int)((p0 / 64) & 3);
-#pragma unroll
-    for (int k = 0; k < 4; k++) ck[k] = (uint32_t)(w[k] >> sh) & 0xFFFFu;
-    B = A.bnd[p0 / 64];
+    ck[0] = (uint32_t)(w0 >> sh) & 0xFFFFu;
+    ck[1] = (uint32_t)(w1 >> sh) & 0xFFFFu;
+    ck[2] = (uint32_t)(w2 >> sh) & 0xFFFFu;
+    ck[3] = (uint32_t)(w3 >> sh) & 0xFFFFu;
+    B = Bw;
   }
   const uint64_t Bk = (tid == 0) ? (B & ~1ull) : B;  // key starts after the tile's first event
   const uint32_t cnt = __popc(ck[0]) + __popc(ck[1]) + __popc(ck[2]) + __popc(ck[3]);
@@ -367,9 +464,9 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const bool staged = tile_total <= kStage;  // block-uniform
   uint64_t o = toff + (excl >> 16);
   uint32_t so = excl >> 16;  // slot within the tile
-  const uint32_t rank0 = A.tile_rank[t] + (excl & 0xFFFF);
-  uint32_t cur_rank = 0xFFFFFFFFu, key = 0;
-  uint64_t kstart = 0;
+  const uint32_t rank0 = trank + (excl & 0xFFFF);
+  uint32_t cur_rank = trank, key = tkey;
+  uint64_t kstart = tkstart;
   // natural order: event p0 + 4 l + k is bit l of ck[k] -> bit 4 l + k
   uint64_t match = spread4(ck[0]) | (spread4(ck[1]) << 1) | (spread4(ck[2]) << 2) | (spread4(ck[3]) << 3);
   while (match) {
@@ -428,9 +525,24 @@ hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n
   return hipGetLastError();
 }
 
+// prefetch depth of stencil_mask's fast path (steps of 256 events whose loads run ahead);
+// CEP_STENCIL_PF (1, 2 or 4) overrides it for measurement
+static int stencil_pf() {
+  static const int pf = [] {
+    const char* e = std::getenv("CEP_STENCIL_PF");
+    const int v = e ? std::atoi(e) : kStDefaultPF;
+    return (v == 1 || v == 2 || v == 4) ? v : kStDefaultPF;
+  }();
+  return pf;
+}
+
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
-  hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
+  const dim3 g((uint32_t)n_tiles), b(kStThreads);
+  const int pf = RANGE ? stencil_pf() : 1;  // only the range fast path streams vector loads
+  if (pf == 4) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 4 : 1>), g, b, 0, st, a);
+  else if (pf == 2) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 2 : 1>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, 1>), g, b, 0, st, a);
   hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }

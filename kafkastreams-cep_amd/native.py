@@ -25,7 +25,7 @@ EXPORTS = [
     "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
-    "cep_batch_layout", "cep_synth_generate_arrival",
+    "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
 ]
 
 
@@ -89,6 +89,8 @@ def lib():
             "cep_synth_generate": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
             "cep_synth_generate_arrival": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
             "cep_batch_layout": ([vp, C.c_int, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_double)], C.c_int),
+            "cep_session_snapshot": ([vp, vp, C.c_size_t, C.POINTER(C.c_size_t)], C.c_int),
+            "cep_session_restore": ([vp, vp, C.c_size_t], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -347,6 +349,19 @@ class Session:
         ms, aux, n = C.c_double(), C.c_double(), C.c_uint32()
         _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(aux), C.byref(n)))
         return ms.value, aux.value, n.value
+
+    def snapshot(self) -> bytes:
+        """The streaming session's complete per-key NFA state as a versioned blob
+        (cep_session_snapshot; the reference's persistent run-queue/buffer stores)."""
+        n = C.c_size_t()
+        _check(lib().cep_session_snapshot(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().cep_session_snapshot(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, blob: bytes) -> None:
+        """Loads a snapshot into this (fresh, streaming) session over the same queries."""
+        _check(lib().cep_session_restore(self.h, blob, len(blob)))
 
     def watermark(self) -> int:
         w = C.c_int64()

@@ -16,7 +16,7 @@ def _irs(bench_only):
 
     irs = [W.stock_query(v).to_ir() for v in ("readme", "test", "demo")]
     irs += [W.strict_abc_query().to_ir(), W.any_kleene_query().to_ir()]
-    irs += [p.to_ir() for p in W.multi_queries(8)]
+    irs += [p.to_ir() for p in W.multi_queries(64)]  # bench.py other_configs (cfg 5); tests use the first 8
     if bench_only:
         return irs
     from fuzz_queries import random_query

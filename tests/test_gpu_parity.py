@@ -256,6 +256,52 @@ def test_streaming_session_batches(query, n_batches, tier):
     np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
 
 
+@pytest.mark.parametrize("query", ["readme", "any_kleene"])
+def test_streaming_snapshot_restore(query):
+    """cep_session_snapshot / cep_session_restore: after every batch the stream's state moves
+    to a brand-new session through a snapshot blob; the merged matches and exceptions equal
+    the oracle's single pass (and the uninterrupted streaming session's)."""
+    import stream_split as SS
+    cfg = W.SynthConfig("t", "stock", 300, 700, 0xCE90000 + 4)
+    off, cols = W.generate(cfg)
+    q = W.stock_query("readme") if query == "readme" else W.any_kleene_query()
+    ir = q.to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    s = N.Session(N.Query(ir), streaming=True, max_runs=64)
+    outs = []
+    for ko, cs in SS.split(off, cols, 4, seed=7):
+        s.push(ko, cs)
+        m = s.matches(0)
+        m["err_code"], m["err_seq"] = s.key_errors(0)
+        outs.append(m)
+        blob = s.snapshot()
+        s.close()
+        s = N.Session(N.Query(ir), streaming=True, max_runs=64)
+        s.restore(blob)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
+def test_snapshot_rejects_mismatch():
+    ir = W.stock_query("readme").to_ir()
+    s = N.Session(N.Query(ir), streaming=True)
+    s.push(np.array([0, 2], np.uint64), [np.array([1, 2], np.int32), np.array([1, 2], np.int32)])
+    blob = s.snapshot()
+    other = N.Session(N.Query(W.any_kleene_query().to_ir()), streaming=True)
+    with pytest.raises(N.CepError):
+        other.restore(blob)  # a different query
+    opts = N.Session(N.Query(ir), streaming=True, max_runs=64)
+    with pytest.raises(N.CepError):
+        opts.restore(blob)  # other ring geometry
+    with pytest.raises(N.CepError):
+        N.Session(N.Query(ir), streaming=True).restore(blob[:40])  # truncated
+    with pytest.raises(N.CepError):
+        N.Session(N.Query(ir)).snapshot()  # not a streaming session
+    fresh = N.Session(N.Query(ir), streaming=True)
+    fresh.restore(blob)
+    assert fresh.snapshot() == blob
+
+
 def test_streaming_rejects_other_key_space():
     s = N.Session(N.Query(W.stock_query("readme").to_ir()), streaming=True)
     s.push(np.array([0, 2], np.uint64), [np.array([1, 2], np.int32), np.array([1, 2], np.int32)])
