@@ -220,6 +220,58 @@ def end_to_end(args, device, dist):
             "matches_per_step": n_m}
 
 
+def ingest(device, steps, keys, cpu_sample):
+    """the step before the matcher.  The cfg-3 stream at `keys` keys x ~1000
+    events as StockEvent JSON record values back to back in HBM (json-simple's serialization,
+    StockEventSerDe.java:75-82), decoded by cep_decode_stock_json (csrc/ingest.hip) into the int32
+    price/volume columns the matcher reads.  Timed with HIP events on the launch stream;
+    algorithmic bytes = record text + 8 B offset read + 4+4+4 B (price, volume, status) written
+    per record.  CPU baseline: oracle/json_oracle.py (the json-simple restatement, 1 thread) on
+    the first `cpu_sample` records."""
+    import torch
+
+    cfg = W.CONFIGS[3]
+    stream = N.synth_stream("stock", cfg.seed, keys, 1000, 0, device)
+    batch = N.StockJsonBatch.synth(stream.cols[0], stream.cols[1], stream.n_events, device)
+    n = stream.n_events
+    out = N.DecodedStock(n, 4, device, name_spans=False)
+    torch.cuda.set_device(device)
+    st = torch.cuda.current_stream()
+    N.decode_stock_json(batch, 4, out, st.cuda_stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        N.decode_stock_json(batch, 4, out, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    bad = int(np.count_nonzero(out.status.download(np.int32, n)))
+    alg = batch.nbytes + 8 * (n + 1) + 12 * n
+    achieved = alg / (ms * 1e-3) / 1e9
+    res = {"workload": f"StockEvent JSON -> int32 columns, cfg3 stream {keys} keys x ~1000 events ({n} records, "
+                       f"{batch.nbytes} bytes)", "value": n / (ms * 1e-3), "unit": "records/s",
+           "ms_per_step": ms, "bytes_per_s": batch.nbytes / (ms * 1e-3), "failed_records": bad,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("decode_stock_json_kernel"),
+                        "kernel": "decode_stock_json_kernel", "algorithmic_bytes": alg}}
+    if cpu_sample:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import json_oracle
+
+        data, off = batch.download()
+        m = min(cpu_sample, n)
+        t0 = time.perf_counter()
+        exp = json_oracle.decode_batch(data[:int(off[m])], off[:m + 1], 4)
+        el = time.perf_counter() - t0
+        _, cols = stream.download()
+        ok = all(e[0] == 0 for e in exp) and [e[1] for e in exp] == cols[0][:m].tolist()
+        res["cpu_baseline"] = {"value": m / el, "unit": "records/s", "cores": 1, "kind": "port",
+                               "sample": f"first {m} records, {el:.2f} s, 1 thread (oracle/json_oracle.py)",
+                               "parity_on_sample": bool(ok)}
+    return res
+
+
 def _partition_ms(s):
     off, perm, ms = N.C.c_void_p(), N.C.c_void_p(), N.C.c_double()
     N._check(N.lib().cep_batch_layout(s.h, N.CEP_MEM_DEVICE, N.C.byref(off), N.C.byref(perm), N.C.byref(ms)))
@@ -240,6 +292,7 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the arrival-order end-to-end figure")
     ap.add_argument("--no-other", action="store_true", help="skip the cfg 4 / cfg 5 figures")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the JSON ingest figure")
     ap.add_argument("--other-keys", type=int, default=100_000, help="keys of the cfg 4 / cfg 5 figures")
     args = ap.parse_args()
 
@@ -302,6 +355,8 @@ def main():
         if dist.world == 1 and not args.no_e2e:
             sess.close()
             out["end_to_end"] = end_to_end(args, device, dist)
+        if dist.world == 1 and not args.no_ingest:
+            out["ingest"] = ingest(device, args.steps, args.other_keys, 0 if args.no_cpu_baseline else 100_000)
         if dist.world == 1 and not args.no_other:
             out["other_configs"] = other_configs(device, max(1, args.steps // 2), 1, dist, args.other_keys)
         print(json.dumps(out), flush=True)

@@ -231,6 +231,32 @@ int cep_device_alloc(int device, size_t bytes, void** out);
 int cep_device_free(void* p);
 int cep_memcpy(void* dst, const void* src, size_t bytes, int dst_memory, int src_memory);
 
+/* ---- ingest: StockEvent JSON record values -> event columns (on the device) ----
+ * Replaces the demo topology's value deserializer StockEventSerDe.JsonSerDeserializer.deserialize
+ * (src/test/java/.../demo/StockEventSerDe.java:58-72: json-simple 1.1.1 JSONParser, then
+ * new StockEvent((String) name, (Long) price, (Long) volume), demo/StockEvent.java:4-14), applied
+ * to a whole batch of record values.  bytes: the values back to back; rec_off[n+1] (u64) their
+ * offsets.  Per record: status[r] = 0 or the CEP_JSON_* exception deserialize() would throw;
+ * price/volume columns (col_width 8 = the reference's long, 4 = the int32 columns the matcher
+ * reads; a long that does not fit is CEP_JSON_NARROW); name_span[2r..2r+1] (optional) = byte
+ * offset of the name's text within the record and its raw length (bit 31: the text holds
+ * escapes), length 0xFFFFFFFF for a null/absent name.  Failed records get 0 in the columns.
+ * All pointers are device memory; the launch is asynchronous on `stream` (hipStream_t, NULL =
+ * the default stream). */
+enum {
+  CEP_JSON_OK = 0,
+  CEP_JSON_PARSE = 1,      /* RuntimeException(ParseException): malformed record */
+  CEP_JSON_CLASS_CAST = 2, /* ClassCastException: not an object, name not a String, price/volume not Long */
+  CEP_JSON_NULL = 3,       /* NullPointerException: null record object, price/volume null or absent */
+  CEP_JSON_NUMBER = 4,     /* NumberFormatException: an integer literal outside long */
+  CEP_JSON_LEX = 5,        /* java.lang.Error from the scanner: an unknown string escape */
+  CEP_JSON_NARROW = 6,     /* col_width 4 and price/volume outside int32 (no reference outcome) */
+  CEP_JSON_DEPTH = 7       /* nesting deeper than 64 (this decoder's limit; the reference parses it) */
+};
+int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_off, uint64_t n_records,
+                          int col_width, void* price, void* volume, int32_t* status, uint32_t* name_span,
+                          void* stream);
+
 /* ---- synthetic workloads (bench / tests): kafkastreams-cep_amd/workloads.py, on device ----
  * kind 0 = "abc" (one int column v = h % 16), 1 = "stock" (int price random walk, int volume).
  * Fills device buffers: key_off [n_keys+1] (u64), cols[0..] (int32, n_events each).
@@ -243,6 +269,11 @@ int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uin
  * of every event in keys_dev [n_events], values in cols_dev. */
 int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
                                uint32_t mean_events, uint32_t* keys_dev, int32_t* const* cols_dev);
+/* StockEvent JSON values of n events as json-simple serializes them (StockEventSerDe.java:75-82),
+ * {"name":"e<i+1>","price":P,"volume":V} (README.md:73-80): rec_off_dev[n+1] and *total (bytes)
+ * are always written; the text goes to out_dev only when *total <= cap. */
+int cep_synth_stock_json(int device, const int32_t* price_dev, const int32_t* volume_dev, uint64_t n,
+                         uint8_t* out_dev, uint64_t cap, uint64_t* rec_off_dev, uint64_t* total);
 
 #ifdef __cplusplus
 }

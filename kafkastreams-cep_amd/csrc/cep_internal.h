@@ -47,6 +47,11 @@ hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n
                             uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd, uint32_t* tile_rank, hipStream_t st);
 hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
 uint64_t stencil_tiles(uint64_t n_events);
+hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
+                                    void* price, void* volume, int32_t* status, uint32_t* name_span,
+                                    hipStream_t st);
+hipError_t synth_stock_json(const int32_t* price, const int32_t* volume, uint64_t n, uint8_t* out, uint64_t cap,
+                            uint64_t* rec_off, uint64_t* total);
 hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, const uint64_t* key_off,
                         int32_t* c0, int32_t* c1, hipStream_t st);
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);

@@ -1,0 +1,164 @@
+// ingest.hip — the step before the matcher: StockEvent JSON records -> event columns.
+//
+// Replaces the demo's value deserializer StockEventSerDe.JsonSerDeserializer.deserialize
+// (test:demo/StockEventSerDe.java:58-72): json-simple 1.1.1's JSONParser (pom.xml:99-104; not in
+// /root/reference, restated here from its published lexer/parser) parses the record, then
+//   new StockEvent((String) o.get("name"), (Long) o.get("price"), (Long) o.get("volume"))
+// (test:demo/StockEvent.java:4-14).  Every record gets the outcome the Java call would have:
+// the columns, or the exception that would escape deserialize() as a status code (CEP_JSON_*).
+//
+// Layout: the batch is Kafka-style record values back to back in HBM (bytes) with u64 record
+// offsets rec_off[n+1].  One thread per record; a 256-record block stages its byte span into
+// LDS with coalesced 16-byte loads and the lanes parse from LDS (a block whose span exceeds
+// the LDS tile parses straight from HBM).  HBM-bound: bytes + 8 B offset read once, the columns
+// and status written once.
+//
+// json-simple semantics reproduced (the parts a StockEvent record can reach):
+//  * lexer (Yylex): whitespace [ \t\n\r\f]; INT -?[0-9]+ -> Long.valueOf (overflow throws
+//    NumberFormatException); DOUBLE INT(\.[0-9]+)?([eE][-+]?[0-9]+)? -> Double; longest match, so
+//    "1." lexes INT then fails on '.'; true/false/null; strings with \" \\ \/ \b \f \n \r \t
+//    \uXXXX escapes and raw bytes otherwise; any other byte outside a string -> ParseException;
+//    an unknown escape -> the scanner's java.lang.Error; a string cut off by the end of input is
+//    end of input.
+//  * parser (JSONParser.parse): commas and colons are skipped wherever they are legal tokens of
+//    the current container state, duplicate keys keep the last value (HashMap.put), one value
+//    then end of input.
+//  * deserialize: the top value must be a JSONObject (null -> NullPointerException on get);
+//    casts and unboxing in argument order: name (String or null), price (Long, unboxed), volume.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "json_parser.h"
+
+namespace cep {
+
+
+
+constexpr int kIngestBlock = 256;
+constexpr uint32_t kIngestLds = 24576;  // bytes of record text staged per block
+
+template <typename T>
+__device__ __forceinline__ void store_cols(void* price, void* volume, uint64_t r, int64_t p, int64_t v) {
+  ((T*)price)[r] = (T)p;
+  ((T*)volume)[r] = (T)v;
+}
+
+__global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
+    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ rec_off, uint64_t n, int col_width,
+    void* __restrict__ price, void* __restrict__ volume, int32_t* __restrict__ status,
+    uint32_t* __restrict__ name_span) {
+  __shared__ uint4 tile[kIngestLds / 16];
+  const uint64_t r0 = (uint64_t)blockIdx.x * kIngestBlock;
+  const uint64_t r1 = r0 + kIngestBlock < n ? r0 + kIngestBlock : n;
+  const uint64_t A = rec_off[r0], B = rec_off[r1];
+  // aligned 16-byte chunks g0..g1 cover the block's span [A, B); a chunk that holds at least one
+  // byte of the span never leaves its pages
+  const uint64_t skew = (uintptr_t)bytes & 15;
+  const uint64_t g0 = (A + skew) >> 4, g1 = (B + skew + 15) >> 4;
+  const bool staged = (g1 - g0) * 16 <= kIngestLds;
+  if (staged) {
+    const uint4* src = (const uint4*)((uintptr_t)bytes - skew);
+    for (uint64_t c = g0 + threadIdx.x; c < g1; c += kIngestBlock) tile[c - g0] = src[c];
+    __syncthreads();
+  }
+  const uint64_t r = r0 + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t a = rec_off[r], b = rec_off[r + 1];
+  json::Parser P;
+  // word view of the record text: LDS tile or HBM
+  const uint8_t* base;
+  if (staged) {
+    base = (const uint8_t*)tile + (a + skew - (g0 << 4));
+  } else {
+    base = bytes + a;
+  }
+  json::parse_record(P, base, (uint32_t)(b - a));
+  int64_t pv, vv;
+  const int32_t st = json::outcome(P, col_width, &pv, &vv);
+  if (col_width == 4) store_cols<int32_t>(price, volume, r, pv, vv);
+  else store_cols<int64_t>(price, volume, r, pv, vv);
+  status[r] = st;
+  if (name_span) json::name_span(P, st, &name_span[2 * r], &name_span[2 * r + 1]);
+}
+
+hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
+                                    void* price, void* volume, int32_t* status, uint32_t* name_span,
+                                    hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_stock_json_kernel, dim3((uint32_t)((n + kIngestBlock - 1) / kIngestBlock)),
+                     dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width, price, volume, status, name_span);
+  return hipGetLastError();
+}
+
+// ---- synthetic records: json-simple's toJSONString of the demo's StockEvent
+// (StockEventSerDe.java:75-82), {"name":"e<i+1>","price":P,"volume":V}, the README's format
+// (README.md:73-80) ----
+
+__device__ __forceinline__ uint32_t ndigits(int64_t v) {
+  uint64_t m = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+  uint32_t d = 1;
+  while (m >= 10) { m /= 10; d++; }
+  return d + (v < 0);
+}
+
+__global__ void __launch_bounds__(256) json_len_kernel(const int32_t* price, const int32_t* volume, uint64_t n,
+                                                       uint64_t* len) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) len[i] = 31 + ndigits((int64_t)i + 1) + ndigits(price[i]) + ndigits(volume[i]);
+}
+
+__device__ __forceinline__ uint64_t put_str(uint8_t* o, uint64_t p, const char* s) {
+  while (*s) o[p++] = (uint8_t)*s++;
+  return p;
+}
+__device__ __forceinline__ uint64_t put_int(uint8_t* o, uint64_t p, int64_t v) {
+  const uint32_t d = ndigits(v);
+  uint64_t m = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+  if (v < 0) o[p] = '-';
+  for (uint32_t k = 0; k < d - (v < 0); k++) {
+    o[p + d - 1 - k] = (uint8_t)('0' + m % 10);
+    m /= 10;
+  }
+  return p + d;
+}
+
+__global__ void __launch_bounds__(256) json_write_kernel(const int32_t* price, const int32_t* volume, uint64_t n,
+                                                         const uint64_t* off, uint8_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t p = off[i];
+  p = put_str(out, p, "{\"name\":\"e");
+  p = put_int(out, p, (int64_t)i + 1);
+  p = put_str(out, p, "\",\"price\":");
+  p = put_int(out, p, price[i]);
+  p = put_str(out, p, ",\"volume\":");
+  p = put_int(out, p, volume[i]);
+  out[p] = '}';
+}
+
+// lengths -> rec_off (inclusive scan into rec_off+1) ; total bytes returned through *total
+hipError_t synth_stock_json(const int32_t* price, const int32_t* volume, uint64_t n, uint8_t* out, uint64_t cap,
+                            uint64_t* rec_off, uint64_t* total) {
+  hipError_t e;
+  if ((e = hipMemset(rec_off, 0, 8)) != hipSuccess) return e;
+  if (n == 0) { *total = 0; return hipSuccess; }
+  const dim3 g((uint32_t)((n + 255) / 256));
+  hipLaunchKernelGGL(json_len_kernel, g, dim3(256), 0, 0, price, volume, n, rec_off + 1);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  size_t tmp = 0;
+  if ((e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp, rec_off + 1, rec_off + 1, (int)n)) != hipSuccess) return e;
+  void* scratch = nullptr;
+  if ((e = hipMalloc(&scratch, tmp + 16)) != hipSuccess) return e;
+  e = hipcub::DeviceScan::InclusiveSum(scratch, tmp, rec_off + 1, rec_off + 1, (int)n);
+  if (e == hipSuccess) e = hipMemcpy(total, rec_off + n, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(scratch);
+  if (e != hipSuccess) return e;
+  if (*total > cap) return hipSuccess;  // caller sees total > cap and retries with more room
+  hipLaunchKernelGGL(json_write_kernel, g, dim3(256), 0, 0, price, volume, n, rec_off, out);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipDeviceSynchronize();
+}
+
+}  // namespace cep

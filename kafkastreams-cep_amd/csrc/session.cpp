@@ -1091,4 +1091,29 @@ int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_k
   });
 }
 
+int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_off, uint64_t n_records,
+                          int col_width, void* price, void* volume, int32_t* status, uint32_t* name_span,
+                          void* stream) {
+  if (!rec_off || !price || !volume || !status || (!bytes && n_records))
+    return fail(CEP_E_INVALID, "null argument");
+  if (col_width != 4 && col_width != 8) return fail(CEP_E_INVALID, "col_width must be 4 or 8");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(launch_decode_stock_json(bytes, rec_off, n_records, col_width, price, volume, status, name_span,
+                                      (hipStream_t)stream));
+  });
+}
+
+int cep_synth_stock_json(int device, const int32_t* price_dev, const int32_t* volume_dev, uint64_t n,
+                         uint8_t* out_dev, uint64_t cap, uint64_t* rec_off_dev, uint64_t* total) {
+  if (!rec_off_dev || !total || (n && (!price_dev || !volume_dev))) return fail(CEP_E_INVALID, "null argument");
+  if (n >= (1ull << 31)) return fail(CEP_E_INVALID, "at most 2^31 - 1 records");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(synth_stock_json(price_dev, volume_dev, n, out_dev, out_dev ? cap : 0, rec_off_dev, total));
+  });
+}
+
 }  // extern "C"

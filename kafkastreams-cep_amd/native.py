@@ -26,6 +26,7 @@ EXPORTS = [
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
+    "cep_decode_stock_json", "cep_synth_stock_json",
 ]
 
 
@@ -91,6 +92,8 @@ def lib():
             "cep_batch_layout": ([vp, C.c_int, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_double)], C.c_int),
             "cep_session_snapshot": ([vp, vp, C.c_size_t, C.POINTER(C.c_size_t)], C.c_int),
             "cep_session_restore": ([vp, vp, C.c_size_t], C.c_int),
+            "cep_decode_stock_json": ([C.c_int, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
+            "cep_synth_stock_json": ([C.c_int, vp, vp, u64, vp, u64, vp, C.POINTER(u64)], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -230,6 +233,72 @@ def synth_arrival_stream(kind: str, seed: int, n_keys: int, mean_events: int, ke
     ptrs = (C.c_void_p * len(cols))(*[c.ptr for c in cols])
     _check(lib().cep_synth_generate_arrival(device, k, seed, n_keys, key_base, mean_events, keys.ptr, ptrs))
     return ArrivalStream(n_keys, n.value, keys, cols, device)
+
+
+class StockJsonBatch:
+    """Record values of the demo's StockEvents topic, back to back in HBM (bytes) with u64 offsets
+    rec_off[n+1]: the input of StockEventSerDe's deserializer (test:demo/StockEventSerDe.java:58-72)
+    for a whole batch."""
+
+    def __init__(self, n, nbytes, data: DeviceBuffer, rec_off: DeviceBuffer, device=0):
+        self.n, self.nbytes, self.data, self.rec_off, self.device = int(n), int(nbytes), data, rec_off, device
+
+    @classmethod
+    def from_records(cls, records, device=0):
+        off = np.zeros(len(records) + 1, np.uint64)
+        off[1:] = np.cumsum([len(r) for r in records], dtype=np.uint64) if records else []
+        blob = np.frombuffer(b"".join(records), np.uint8)
+        d = DeviceBuffer(max(1, blob.nbytes), device)
+        if blob.nbytes:
+            d.upload(blob)
+        o = DeviceBuffer(off.nbytes, device)
+        o.upload(off)
+        return cls(len(records), blob.nbytes, d, o, device)
+
+    @classmethod
+    def synth(cls, price: DeviceBuffer, volume: DeviceBuffer, n: int, device=0):
+        """json-simple's serialization of n StockEvents e1..en (csrc/ingest.hip), made in HBM."""
+        o = DeviceBuffer(8 * (n + 1), device)
+        tot = C.c_uint64()
+        _check(lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, None, 0, o.ptr, C.byref(tot)))
+        d = DeviceBuffer(max(1, tot.value), device)
+        _check(lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, d.ptr, tot.value, o.ptr, C.byref(tot)))
+        return cls(n, tot.value, d, o, device)
+
+    def download(self):
+        return bytes(self.data.download(np.uint8, self.nbytes)), self.rec_off.download(np.uint64, self.n + 1)
+
+
+class DecodedStock:
+    """Device columns of a decoded StockJsonBatch (price, volume, status, name spans)."""
+
+    def __init__(self, n, col_width, device=0, name_spans=True):
+        self.n, self.col_width = int(n), int(col_width)
+        self.price = DeviceBuffer(col_width * max(1, n), device)
+        self.volume = DeviceBuffer(col_width * max(1, n), device)
+        self.status = DeviceBuffer(4 * max(1, n), device)
+        self.name_span = DeviceBuffer(8 * max(1, n), device) if name_spans else None
+
+    def download(self):
+        dt = np.int32 if self.col_width == 4 else np.int64
+        out = {"price": self.price.download(dt, self.n), "volume": self.volume.download(dt, self.n),
+               "status": self.status.download(np.int32, self.n)}
+        if self.name_span is not None:
+            out["name_span"] = self.name_span.download(np.uint32, 2 * self.n).reshape(-1, 2)
+        return out
+
+
+def decode_stock_json(batch: StockJsonBatch, col_width: int = 8, out: DecodedStock | None = None,
+                      stream=None, name_spans=True) -> DecodedStock:
+    """cep_decode_stock_json: one launch over the batch (asynchronous on `stream`, a hipStream_t
+    handle or None for the default stream)."""
+    if out is None:
+        out = DecodedStock(batch.n, col_width, batch.device, name_spans)
+    assert out.n == batch.n and out.col_width == col_width
+    _check(lib().cep_decode_stock_json(batch.device, batch.data.ptr, batch.rec_off.ptr, batch.n, col_width,
+                                       out.price.ptr, out.volume.ptr, out.status.ptr,
+                                       out.name_span.ptr if out.name_span is not None else None, stream))
+    return out
 
 
 class Session:

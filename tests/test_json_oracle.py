@@ -1,0 +1,64 @@
+"""CPU checks of the JSON ingest oracle (oracle/json_oracle.py): the README demo records decode
+to the README's values (README.md:73-80, the one reference fixture) and re-serialize to the same
+bytes (StockEventSerDe.java:75-82); the hand-written json-simple cases give their outcomes."""
+import json_cases as JC
+import pytest
+
+import json_oracle as J
+
+
+def test_readme_records_decode():
+    for rec, price, vol in JC.README:
+        st, p, v, span = J.deserialize(rec)
+        assert (st, p, v) == (J.OK, price, vol)
+        off, ln, esc = span
+        name = rec[off:off + ln]
+        assert J.serialize(name.decode(), p, v) == rec and not esc
+
+
+@pytest.mark.parametrize("rec,code", JC.CASES)
+def test_case_outcomes(rec, code):
+    assert J.deserialize(rec)[0] == code, rec
+
+
+def test_narrow_for_int32_columns():
+    assert J.deserialize(b'{"price":3000000000,"volume":2}', 4)[0] == J.NARROW
+    assert J.deserialize(b'{"price":-2147483648,"volume":2147483647}', 4)[:3] == (J.OK, -(1 << 31), (1 << 31) - 1)
+
+
+def test_deep_nesting_parses_in_reference():
+    # json-simple has no depth limit; the GPU decoder stops at 64 (CEP_JSON_DEPTH, documented)
+    assert J.deserialize(JC.deep(100))[0] == J.OK
+
+
+def test_fuzz_covers_every_outcome():
+    seen = {J.deserialize(r)[0] for r in JC.fuzz(1, 4000)}
+    assert {J.OK, J.PARSE, J.CLASS_CAST, J.NULL} <= seen
+
+
+# ---- the GPU decoder's state machine, compiled for the host (tests/json_cpu.py) ----
+
+import json_cpu  # noqa: E402
+import numpy as np  # noqa: E402
+
+
+def _same(records, col_width=8):
+    got = json_cpu.decode(records, col_width)
+    exp = json_cpu.oracle_arrays([J.deserialize(r, col_width) for r in records])
+    for g, e, what in zip(got, exp, ("status", "price", "volume", "name_span")):
+        bad = np.nonzero((g != e).reshape(len(records), -1).any(axis=1))[0]
+        assert len(bad) == 0, (what, [(records[i], g[i], e[i]) for i in bad[:5]])
+
+
+def test_lane_parser_cases():
+    _same([c for c, _ in JC.CASES] + [r for r, _, _ in JC.README])
+    _same([c for c, _ in JC.CASES], col_width=4)
+
+
+def test_lane_parser_fuzz():
+    _same(JC.fuzz(7, 20000))
+
+
+def test_lane_parser_depth_limit():
+    st = json_cpu.decode([JC.deep(63), JC.deep(64)])[0]
+    assert st.tolist() == [J.OK, J.DEPTH]  # 64 levels incl. the record object; deeper is CEP_JSON_DEPTH (documented)
