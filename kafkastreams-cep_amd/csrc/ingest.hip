@@ -67,14 +67,16 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
   if (r >= n) return;
   const uint64_t a = rec_off[r], b = rec_off[r + 1];
   json::Parser P;
-  // word view of the record text: LDS tile or HBM
-  const uint8_t* base;
+  const uint32_t len = (uint32_t)(b - a);
   if (staged) {
-    base = (const uint8_t*)tile + (a + skew - (g0 << 4));
+    // LDS: 32-bit byte offset into the tile, words read with ds_read (no flat pointer into LDS)
+    const uint32_t o = (uint32_t)(a + skew - (g0 << 4));
+    const uint32_t* tw = (const uint32_t*)tile;
+    const uint32_t w0 = o >> 2;
+    json::parse_words(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
   } else {
-    base = bytes + a;
+    json::parse_record(P, bytes + a, len);
   }
-  json::parse_record(P, base, (uint32_t)(b - a));
   int64_t pv, vv;
   const int32_t st = json::outcome(P, col_width, &pv, &vv);
   if (col_width == 4) store_cols<int32_t>(price, volume, r, pv, vv);

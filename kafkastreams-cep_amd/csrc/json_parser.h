@@ -16,10 +16,10 @@ enum Par : uint8_t { P_INIT, P_FIN, P_OBJ, P_KEY, P_ARR };
 enum Kind : uint8_t { K_ABSENT, K_STRING, K_INT, K_DOUBLE, K_BOOL, K_NULL, K_OBJECT, K_ARRAY };
 constexpr int kMaxDepth = 64;
 
-__device__ __forceinline__ uint8_t target_char(int t, int i) {
-  // "name", "price", "volume"
-  const char* s = t == 0 ? "name" : (t == 1 ? "price" : "volume");
-  return (uint8_t)s[i];
+// "name", "price", "volume" as little-endian byte packs (registers, no literal-table loads)
+__device__ __forceinline__ uint32_t target_char(int t, int i) {
+  const uint64_t k = t == 0 ? 0x656D616Eull : (t == 1 ? 0x6563697270ull : 0x656D756C6F76ull);
+  return (uint32_t)(k >> (8 * i)) & 0xFF;
 }
 __device__ __forceinline__ int target_len(int t) { return t == 0 ? 4 : (t == 1 ? 5 : 6); }
 
@@ -52,8 +52,8 @@ struct Parser {
   uint8_t top_kind = K_ABSENT;
   int8_t cur_key = -1;  // target id of the pending top-level key
   // the three fields (last value wins)
-  uint8_t kind[3] = {K_ABSENT, K_ABSENT, K_ABSENT};
-  int64_t val[3] = {0, 0, 0};
+  uint8_t kind0 = K_ABSENT, kind1 = K_ABSENT, kind2 = K_ABSENT;  // name, price, volume
+  int64_t val1 = 0, val2 = 0;
   uint32_t name_off = 0, name_len = 0;
   bool name_esc = false;
 
@@ -113,8 +113,9 @@ struct Parser {
         if (tok == 'v' || tok == '{' || tok == '[') {
           if (cur_key >= 0) {
             const uint8_t k = tok == 'v' ? vkind : (tok == '{' ? K_OBJECT : K_ARRAY);
-            kind[cur_key] = k;
-            val[cur_key] = v;
+            if (cur_key == 0) kind0 = k;
+            else if (cur_key == 1) { kind1 = k; val1 = v; }
+            else { kind2 = k; val2 = v; }
             if (cur_key == 0) { name_off = so; name_len = sl; name_esc = sesc; }
           }
           if (tok == 'v') par = P_OBJ;
@@ -209,10 +210,10 @@ struct Parser {
         return;
       }
       case L_LIT: {
-        const char* s = lit == 0 ? "true" : (lit == 1 ? "false" : "null");
-        if ((uint8_t)s[lit_pos] != c) { fail(CEP_JSON_PARSE); return; }  // only "." matched at the start
+        const uint64_t s = lit == 0 ? 0x65757274ull : (lit == 1 ? 0x65736C6166ull : 0x6C6C756Eull);  // true false null
+        if (((s >> (8 * lit_pos)) & 0xFF) != c) { fail(CEP_JSON_PARSE); return; }  // only "." matched at the start
         lit_pos++;
-        if (s[lit_pos] == 0) {
+        if (((s >> (8 * lit_pos)) & 0xFF) == 0) {
           lex = L_WS;
           token('v', lit == 2 ? K_NULL : K_BOOL, 0, 0, 0, false, -1);
         }
@@ -277,32 +278,39 @@ struct Parser {
     if (status) return;
     if (top_kind == K_NULL) { status = CEP_JSON_NULL; return; }  // ((JSONObject) null).get
     if (top_kind != K_OBJECT) { status = CEP_JSON_CLASS_CAST; return; }
-    if (kind[0] != K_ABSENT && kind[0] != K_NULL && kind[0] != K_STRING) { status = CEP_JSON_CLASS_CAST; return; }
+    if (kind0 != K_ABSENT && kind0 != K_NULL && kind0 != K_STRING) { status = CEP_JSON_CLASS_CAST; return; }
     for (int f = 1; f < 3; f++) {
-      if (kind[f] == K_ABSENT || kind[f] == K_NULL) { status = CEP_JSON_NULL; return; }
-      if (kind[f] != K_INT) { status = CEP_JSON_CLASS_CAST; return; }
+      const uint8_t kf = f == 1 ? kind1 : kind2;
+      if (kf == K_ABSENT || kf == K_NULL) { status = CEP_JSON_NULL; return; }
+      if (kf != K_INT) { status = CEP_JSON_CLASS_CAST; return; }
     }
   }
 };
 
-// parse one record whose text starts at `base` (len bytes), reading aligned 32-bit words (an
-// aligned word holding a byte of the record never leaves the record's pages)
-__device__ __forceinline__ void parse_record(Parser& P, const uint8_t* base, uint32_t len) {
-  const uint32_t* words = (const uint32_t*)((uintptr_t)base & ~(uintptr_t)3);
-  const uint32_t lead = (uint32_t)((uintptr_t)base & 3);
+// parse one record of len bytes whose first byte is byte `lead` (0..3) of word(0); word(j) returns
+// the record's j-th aligned 32-bit word (an aligned word holding a byte of the record never
+// leaves the record's pages)
+template <typename Word>
+__device__ __forceinline__ void parse_words(Parser& P, Word word, uint32_t lead, uint32_t len) {
   uint32_t i = 0;
   while (i < len && !P.done) {
-    const uint32_t w = words[(i + lead) >> 2];
+    const uint32_t w = word((i + lead) >> 2);
     uint32_t k = (i + lead) & 3;
     for (; k < 4 && i < len && !P.done; k++, i++) P.feed((uint8_t)(w >> (8 * k)), i);
   }
   if (!P.done) P.finish();
 }
 
+// the record at `base` in flat memory
+__device__ __forceinline__ void parse_record(Parser& P, const uint8_t* base, uint32_t len) {
+  const uint32_t* words = (const uint32_t*)((uintptr_t)base & ~(uintptr_t)3);
+  parse_words(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)base & 3), len);
+}
+
 // the record's outcome for col_width-byte columns: status, and price/volume (0 on failure)
 __device__ __forceinline__ int32_t outcome(const Parser& P, int col_width, int64_t* price, int64_t* volume) {
   int32_t st = P.status;
-  int64_t pv = P.val[1], vv = P.val[2];
+  int64_t pv = P.val1, vv = P.val2;
   if (st == 0 && col_width == 4 && (pv < INT32_MIN || pv > INT32_MAX || vv < INT32_MIN || vv > INT32_MAX))
     st = CEP_JSON_NARROW;
   if (st) pv = vv = 0;
@@ -313,7 +321,7 @@ __device__ __forceinline__ int32_t outcome(const Parser& P, int col_width, int64
 
 // name span: offset and raw length of the name's text (bit 31: escapes), 0xFFFFFFFF if null/absent
 __device__ __forceinline__ void name_span(const Parser& P, int32_t st, uint32_t* off, uint32_t* len) {
-  const bool has = st == 0 && P.kind[0] == K_STRING;
+  const bool has = st == 0 && P.kind0 == K_STRING;
   *off = has ? P.name_off : 0;
   *len = has ? (P.name_len | (P.name_esc ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
 }

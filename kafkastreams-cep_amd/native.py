@@ -298,6 +298,7 @@ def decode_stock_json(batch: StockJsonBatch, col_width: int = 8, out: DecodedSto
     _check(lib().cep_decode_stock_json(batch.device, batch.data.ptr, batch.rec_off.ptr, batch.n, col_width,
                                        out.price.ptr, out.volume.ptr, out.status.ptr,
                                        out.name_span.ptr if out.name_span is not None else None, stream))
+    out._src = batch  # the launch is asynchronous: keep the input's device buffers alive with the output
     return out
 
 
