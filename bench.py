@@ -15,7 +15,8 @@ Prints ONE JSON line on rank 0 (contract in the task statement; fields documente
 DESIGN.md §7).  `roofline` prices cep_nfa_jit at SURVEY §8(d)'s algorithmic bytes (columns read
 once + 4 B per emitted event id + 4 B per match) against 8 TB/s; `cpu_baseline` times the
 oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/8 key
-sample on this host's cores.
+sample on this host's cores.  `ingest` is the JSON decoder (csrc/ingest.hip) on the cfg-3
+stream serialized as StockEvent records, with its own roofline and CPU baseline.
 """
 import argparse
 import json
@@ -228,24 +229,30 @@ def ingest(device, steps, keys, cpu_sample):
     algorithmic bytes = record text + 8 B offset read + 4+4+4 B (price, volume, status) written
     per record.  CPU baseline: oracle/json_oracle.py (the json-simple restatement, 1 thread) on
     the first `cpu_sample` records."""
-    import torch
+    import ctypes as C
 
+    hip = C.CDLL("libamdhip64.so")
     cfg = W.CONFIGS[3]
     stream = N.synth_stream("stock", cfg.seed, keys, 1000, 0, device)
     batch = N.StockJsonBatch.synth(stream.cols[0], stream.cols[1], stream.n_events, device)
     n = stream.n_events
     out = N.DecodedStock(n, 4, device, name_spans=False)
-    torch.cuda.set_device(device)
-    st = torch.cuda.current_stream()
-    N.decode_stock_json(batch, 4, out, st.cuda_stream)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
+    # HIP events on the stream the kernel is launched on (the null stream)
+    e0, e1 = C.c_void_p(), C.c_void_p()
+    assert hip.hipSetDevice(device) == 0 and hip.hipEventCreate(C.byref(e0)) == 0
+    assert hip.hipEventCreate(C.byref(e1)) == 0
+    N.decode_stock_json(batch, 4, out, None)
+    assert hip.hipDeviceSynchronize() == 0
+    hip.hipEventRecord(e0, None)
     for _ in range(steps):
-        N.decode_stock_json(batch, 4, out, st.cuda_stream)
-    e1.record(st)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+        N.decode_stock_json(batch, 4, out, None)
+    hip.hipEventRecord(e1, None)
+    assert hip.hipEventSynchronize(e1) == 0
+    f = C.c_float()
+    assert hip.hipEventElapsedTime(C.byref(f), e0, e1) == 0
+    hip.hipEventDestroy(e0)
+    hip.hipEventDestroy(e1)
+    ms = f.value / steps
     bad = int(np.count_nonzero(out.status.download(np.int32, n)))
     alg = batch.nbytes + 8 * (n + 1) + 12 * n
     achieved = alg / (ms * 1e-3) / 1e9

@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
     const uint32_t o = (uint32_t)(a + skew - (g0 << 4));
     const uint32_t* tw = (const uint32_t*)tile;
     const uint32_t w0 = o >> 2;
-    json::parse_words(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
+    json::parse_any(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
   } else {
     json::parse_record(P, bytes + a, len);
   }

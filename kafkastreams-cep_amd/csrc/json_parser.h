@@ -301,10 +301,72 @@ __device__ __forceinline__ void parse_words(Parser& P, Word word, uint32_t lead,
   if (!P.done) P.finish();
 }
 
+// Fast path for the serializer's own layout, {"name":"<text without \" or \\>","price":<int>,"volume":<int>}
+// with at most 18 digits per number (StockEventSerDe.java:75-82, the README's records): a straight
+// scan every lane of a wave runs in step.  On success P holds exactly what the state machine
+// would produce for that record; anything else returns false with P untouched and takes the
+// general path.
+template <typename Word>
+__device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, uint32_t len) {
+  if (len < 31) return false;
+  uint32_t cj = 0xFFFFFFFFu, cw = 0;
+  auto byte = [&](uint32_t i) -> uint32_t {
+    const uint32_t p = i + lead, j = p >> 2;
+    if (j != cj) { cj = j; cw = word(j); }
+    return (cw >> (8 * (p & 3))) & 0xFF;
+  };
+  auto lit = [&](uint32_t& i, uint64_t pack, int n) -> bool {  // n <= 8 bytes, little-endian pack
+    bool ok = i + n <= len;
+    for (int k = 0; k < n && ok; k++) ok = byte(i + k) == ((pack >> (8 * k)) & 0xFF);
+    i += n;
+    return ok;
+  };
+  auto num = [&](uint32_t& i, int64_t& v) -> bool {
+    const bool neg = i < len && byte(i) == '-';
+    i += neg;
+    uint64_t m = 0;
+    int nd = 0;
+    while (i < len && nd <= 18) {
+      const uint32_t c = byte(i);
+      if (c - '0' > 9u) break;
+      m = m * 10 + (c - '0');
+      nd++;
+      i++;
+    }
+    v = neg ? -(int64_t)m : (int64_t)m;
+    return nd >= 1 && nd <= 18;
+  };
+  uint32_t i = 0;
+  if (byte(0) != '{' || (i = 1, !lit(i, 0x22656D616E22ull, 6)) || !lit(i, 0x223A, 2)) return false;  // {"name":"
+  const uint32_t n0 = i;
+  for (;; i++) {
+    if (i >= len) return false;
+    const uint32_t c = byte(i);
+    if (c == '"') break;
+    if (c == '\\') return false;
+  }
+  const uint32_t nl = i - n0;
+  i++;
+  int64_t pv, vv;
+  if (!lit(i, 0x226563697270222Cull, 8) || !lit(i, 0x3A, 1) || !num(i, pv)) return false;  // ,"price":
+  if (!lit(i, 0x6D756C6F76222Cull, 7) || !lit(i, 0x3A2265, 3) || !num(i, vv)) return false;  // ,"volume":
+  if (i + 1 != len || byte(i) != '}') return false;
+  P.kind0 = K_STRING; P.name_off = n0; P.name_len = nl; P.name_esc = false;
+  P.kind1 = K_INT; P.val1 = pv; P.kind2 = K_INT; P.val2 = vv;
+  P.status = 0; P.done = true;
+  return true;
+}
+
+// a record: the fast path, else the general state machine
+template <typename Word>
+__device__ __forceinline__ void parse_any(Parser& P, Word word, uint32_t lead, uint32_t len) {
+  if (!parse_fast(P, word, lead, len)) parse_words(P, word, lead, len);
+}
+
 // the record at `base` in flat memory
 __device__ __forceinline__ void parse_record(Parser& P, const uint8_t* base, uint32_t len) {
   const uint32_t* words = (const uint32_t*)((uintptr_t)base & ~(uintptr_t)3);
-  parse_words(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)base & 3), len);
+  parse_any(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)base & 3), len);
 }
 
 // the record's outcome for col_width-byte columns: status, and price/volume (0 on failure)

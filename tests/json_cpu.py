@@ -51,3 +51,11 @@ def oracle_arrays(results):
     span = np.array([(0, 0xFFFFFFFF) if r[3] is None else (r[3][0], r[3][1] | (r[3][2] << 31)) for r in results],
                     np.uint32).reshape(-1, 2)
     return st, price, vol, span
+
+
+def fast_path(record: bytes):
+    """(takes the fast path, fast and general paths agree) for one record."""
+    buf, _ = pack([record])
+    ok = C.c_int()
+    f = lib().json_cpu_fast_agrees(C.c_void_p(buf.ctypes.data + 8), C.c_uint32(len(record)), C.byref(ok))
+    return bool(f), bool(ok.value)

@@ -14,3 +14,20 @@ extern "C" void json_cpu_decode(const uint8_t* bytes, const uint64_t* rec_off, u
     cep::json::name_span(P, status[r], &span[2 * r], &span[2 * r + 1]);
   }
 }
+
+// 1 if the record takes the fast path; its outcome and the general state machine's must agree
+extern "C" int json_cpu_fast_agrees(const uint8_t* rec, uint32_t len, int* agrees) {
+  const uint32_t* words = (const uint32_t*)((uintptr_t)rec & ~(uintptr_t)3);
+  auto w = [words](uint32_t j) { return words[j]; };
+  const uint32_t lead = (uint32_t)((uintptr_t)rec & 3);
+  cep::json::Parser F, G;
+  const int fast = cep::json::parse_fast(F, w, lead, len);
+  cep::json::parse_words(G, w, lead, len);
+  int64_t fp, fv, gp, gv;
+  uint32_t fo, fl, go, gl;
+  const int32_t fs = cep::json::outcome(F, 8, &fp, &fv), gs = cep::json::outcome(G, 8, &gp, &gv);
+  cep::json::name_span(F, fs, &fo, &fl);
+  cep::json::name_span(G, gs, &go, &gl);
+  *agrees = !fast || (fs == gs && fp == gp && fv == gv && fo == go && fl == gl);
+  return fast;
+}

@@ -62,3 +62,15 @@ def test_lane_parser_fuzz():
 def test_lane_parser_depth_limit():
     st = json_cpu.decode([JC.deep(63), JC.deep(64)])[0]
     assert st.tolist() == [J.OK, J.DEPTH]  # 64 levels incl. the record object; deeper is CEP_JSON_DEPTH (documented)
+
+
+def test_fast_path_taken_for_serializer_records_and_exact():
+    canon = [J.serialize("e%d" % i, p, v) for i, (p, v) in enumerate(
+        [(1, 2), (-5, 0), (123456789012345678, -999999999999999999), (120, 1010)])] + [r for r, _, _ in JC.README]
+    assert all(json_cpu.fast_path(r) == (True, True) for r in canon)
+    # 19-digit numbers, escapes, other layouts: general path
+    for r in (J.serialize("e", 1234567890123456789, 1), b'{"name":"a\\"b","price":1,"volume":2}',
+              b'{"price":1,"volume":2,"name":"a"}', b'{"name":"a","price":1,"volume":2} '):
+        assert json_cpu.fast_path(r)[0] is False
+    for r in [c for c, _ in JC.CASES] + JC.fuzz(5, 5000):
+        assert json_cpu.fast_path(r)[1], r
