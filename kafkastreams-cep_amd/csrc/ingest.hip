@@ -8,9 +8,11 @@
 // the columns, or the exception that would escape deserialize() as a status code (CEP_JSON_*).
 //
 // Layout: the batch is Kafka-style record values back to back in HBM (bytes) with u64 record
-// offsets rec_off[n+1].  One thread per record; a 256-record block stages its byte span into
-// LDS with coalesced 16-byte loads and the lanes parse from LDS (a block whose span exceeds
-// the LDS tile parses straight from HBM).  HBM-bound: bytes + 8 B offset read once, the columns
+// offsets rec_off[n+1].  One thread per record, two passes.  Pass 1 (decode_stock_json_kernel,
+// 24 VGPRs): a 256-record block stages its byte span into LDS with coalesced 16-byte loads
+// (a block whose span exceeds the tile reads HBM) and every lane runs the serializer-layout fast
+// path; records it cannot take are marked pending.  Pass 2 (decode_stock_json_general) runs
+// the full state machine on the pending records only.  HBM-bound: bytes + 8 B offset read once, the columns
 // and status written once.
 //
 // json-simple semantics reproduced (the parts a StockEvent record can reach):
@@ -37,7 +39,8 @@ namespace cep {
 
 
 constexpr int kIngestBlock = 256;
-constexpr uint32_t kIngestLds = 24576;  // bytes of record text staged per block
+constexpr uint32_t kIngestLds = 16384;  // bytes of record text staged per block (avg record <= 64 B)
+constexpr int32_t kPending = -1;          // pass 1 left the record to the general state machine
 
 template <typename T>
 __device__ __forceinline__ void store_cols(void* price, void* volume, uint64_t r, int64_t p, int64_t v) {
@@ -45,6 +48,17 @@ __device__ __forceinline__ void store_cols(void* price, void* volume, uint64_t r
   ((T*)volume)[r] = (T)v;
 }
 
+__device__ __forceinline__ void write_outcome(const json::Parser& P, uint64_t r, int col_width, void* price,
+                                              void* volume, int32_t* status, uint32_t* name_span) {
+  int64_t pv, vv;
+  const int32_t st = json::outcome(P, col_width, &pv, &vv);
+  if (col_width == 4) store_cols<int32_t>(price, volume, r, pv, vv);
+  else store_cols<int64_t>(price, volume, r, pv, vv);
+  status[r] = st;
+  if (name_span) json::name_span(P, st, &name_span[2 * r], &name_span[2 * r + 1]);
+}
+
+// Pass 1: each 256-record block staged in LDS, the serializer-layout fast path per lane.
 __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
     const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ rec_off, uint64_t n, int col_width,
     void* __restrict__ price, void* __restrict__ volume, int32_t* __restrict__ status,
@@ -68,29 +82,48 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
   const uint64_t a = rec_off[r], b = rec_off[r + 1];
   json::Parser P;
   const uint32_t len = (uint32_t)(b - a);
+  bool fast;
   if (staged) {
     // LDS: 32-bit byte offset into the tile, words read with ds_read (no flat pointer into LDS)
     const uint32_t o = (uint32_t)(a + skew - (g0 << 4));
     const uint32_t* tw = (const uint32_t*)tile;
     const uint32_t w0 = o >> 2;
-    json::parse_any(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
+    fast = json::parse_fast(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
   } else {
-    json::parse_record(P, bytes + a, len);
+    const uint32_t* words = (const uint32_t*)((uintptr_t)(bytes + a) & ~(uintptr_t)3);
+    fast = json::parse_fast(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3), len);
   }
-  int64_t pv, vv;
-  const int32_t st = json::outcome(P, col_width, &pv, &vv);
-  if (col_width == 4) store_cols<int32_t>(price, volume, r, pv, vv);
-  else store_cols<int64_t>(price, volume, r, pv, vv);
-  status[r] = st;
-  if (name_span) json::name_span(P, st, &name_span[2 * r], &name_span[2 * r + 1]);
+  if (!fast) {
+    status[r] = kPending;
+    return;
+  }
+  write_outcome(P, r, col_width, price, volume, status, name_span);
+}
+
+// Pass 2: the records pass 1 could not take, through the general state machine (from HBM).
+__global__ void __launch_bounds__(kIngestBlock) decode_stock_json_general(
+    const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ rec_off, uint64_t n, int col_width,
+    void* __restrict__ price, void* __restrict__ volume, int32_t* __restrict__ status,
+    uint32_t* __restrict__ name_span) {
+  const uint64_t r = (uint64_t)blockIdx.x * kIngestBlock + threadIdx.x;
+  if (r >= n || status[r] != kPending) return;
+  const uint64_t a = rec_off[r], b = rec_off[r + 1];
+  const uint32_t* words = (const uint32_t*)((uintptr_t)(bytes + a) & ~(uintptr_t)3);
+  json::Parser P;
+  json::parse_words(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3),
+                    (uint32_t)(b - a));
+  write_outcome(P, r, col_width, price, volume, status, name_span);
 }
 
 hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
                                     void* price, void* volume, int32_t* status, uint32_t* name_span,
                                     hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_stock_json_kernel, dim3((uint32_t)((n + kIngestBlock - 1) / kIngestBlock)),
-                     dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width, price, volume, status, name_span);
+  const dim3 grid((uint32_t)((n + kIngestBlock - 1) / kIngestBlock));
+  hipLaunchKernelGGL(decode_stock_json_kernel, grid, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width, price,
+                     volume, status, name_span);
+  hipLaunchKernelGGL(decode_stock_json_general, grid, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width,
+                     price, volume, status, name_span);
   return hipGetLastError();
 }
 
