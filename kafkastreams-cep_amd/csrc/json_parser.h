@@ -315,9 +315,18 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
     if (j != cj) { cj = j; cw = word(j); }
     return (cw >> (8 * (p & 3))) & 0xFF;
   };
+  // bytes i..i+3 as one little-endian word (only called with i + 4 <= len: no read past the record)
+  auto get4 = [&](uint32_t i) -> uint32_t {
+    const uint32_t p = i + lead, j = p >> 2, sh = p & 3;
+    const uint32_t lo = word(j);
+    if (!sh) return lo;
+    return (uint32_t)((((uint64_t)word(j + 1) << 32) | lo) >> (8 * sh));
+  };
   auto lit = [&](uint32_t& i, uint64_t pack, int n) -> bool {  // n <= 8 bytes, little-endian pack
     bool ok = i + n <= len;
-    for (int k = 0; k < n && ok; k++) ok = byte(i + k) == ((pack >> (8 * k)) & 0xFF);
+    int k = 0;
+    for (; k + 4 <= n && ok; k += 4) ok = get4(i + k) == (uint32_t)(pack >> (8 * k));
+    for (; k < n && ok; k++) ok = byte(i + k) == ((pack >> (8 * k)) & 0xFF);
     i += n;
     return ok;
   };
@@ -337,7 +346,7 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
     return nd >= 1 && nd <= 18;
   };
   uint32_t i = 0;
-  if (byte(0) != '{' || (i = 1, !lit(i, 0x22656D616E22ull, 6)) || !lit(i, 0x223A, 2)) return false;  // {"name":"
+  if (!lit(i, 0x3A22656D616E227Bull, 8) || !lit(i, 0x22, 1)) return false;  // {"name":"
   const uint32_t n0 = i;
   for (;; i++) {
     if (i >= len) return false;
@@ -349,7 +358,7 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
   i++;
   int64_t pv, vv;
   if (!lit(i, 0x226563697270222Cull, 8) || !lit(i, 0x3A, 1) || !num(i, pv)) return false;  // ,"price":
-  if (!lit(i, 0x6D756C6F76222Cull, 7) || !lit(i, 0x3A2265, 3) || !num(i, vv)) return false;  // ,"volume":
+  if (!lit(i, 0x656D756C6F76222Cull, 8) || !lit(i, 0x3A22, 2) || !num(i, vv)) return false;  // ,"volume":
   if (i + 1 != len || byte(i) != '}') return false;
   P.kind0 = K_STRING; P.name_off = n0; P.name_len = nl; P.name_esc = false;
   P.kind1 = K_INT; P.val1 = pv; P.kind2 = K_INT; P.val2 = vv;
