@@ -261,7 +261,8 @@ def ingest(device, steps, keys, cpu_sample):
            "ms_per_step": ms, "bytes_per_s": batch.nbytes / (ms * 1e-3), "failed_records": bad,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("decode_stock_json_kernel"),
-                        "kernel": "decode_stock_json_kernel", "algorithmic_bytes": alg}}
+                        "kernel": "decode_stock_json_kernel (+ decode_stock_json_general over pending records)",
+                        "algorithmic_bytes": alg}}
     if cpu_sample:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import json_oracle
