@@ -105,14 +105,21 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_general(
     const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ rec_off, uint64_t n, int col_width,
     void* __restrict__ price, void* __restrict__ volume, int32_t* __restrict__ status,
     uint32_t* __restrict__ name_span) {
-  const uint64_t r = (uint64_t)blockIdx.x * kIngestBlock + threadIdx.x;
-  if (r >= n || status[r] != kPending) return;
-  const uint64_t a = rec_off[r], b = rec_off[r + 1];
-  const uint32_t* words = (const uint32_t*)((uintptr_t)(bytes + a) & ~(uintptr_t)3);
-  json::Parser P;
-  json::parse_words(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3),
-                    (uint32_t)(b - a));
-  write_outcome(P, r, col_width, price, volume, status, name_span);
+  // 4 records per thread: the status scan is the whole pass when nothing is pending
+  const uint64_t r4 = ((uint64_t)blockIdx.x * kIngestBlock + threadIdx.x) * 4;
+  int32_t st4[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) st4[k] = r4 + k < n ? status[r4 + k] : 0;
+  for (int k = 0; k < 4; k++) {
+    if (st4[k] != kPending) continue;
+    const uint64_t r = r4 + k;
+    const uint64_t a = rec_off[r], b = rec_off[r + 1];
+    const uint32_t* words = (const uint32_t*)((uintptr_t)(bytes + a) & ~(uintptr_t)3);
+    json::Parser P;
+    json::parse_words(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3),
+                      (uint32_t)(b - a));
+    write_outcome(P, r, col_width, price, volume, status, name_span);
+  }
 }
 
 hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
@@ -122,7 +129,8 @@ hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_of
   const dim3 grid((uint32_t)((n + kIngestBlock - 1) / kIngestBlock));
   hipLaunchKernelGGL(decode_stock_json_kernel, grid, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width, price,
                      volume, status, name_span);
-  hipLaunchKernelGGL(decode_stock_json_general, grid, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width,
+  const dim3 grid2((uint32_t)((n + 4 * kIngestBlock - 1) / (4 * kIngestBlock)));
+  hipLaunchKernelGGL(decode_stock_json_general, grid2, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width,
                      price, volume, status, name_span);
   return hipGetLastError();
 }
