@@ -348,11 +348,19 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
   uint32_t i = 0;
   if (!lit(i, 0x3A22656D616E227Bull, 8) || !lit(i, 0x22, 1)) return false;  // {"name":"
   const uint32_t n0 = i;
-  for (;; i++) {
-    if (i >= len) return false;
+  for (;;) {  // the name's closing quote: four bytes at a time (SWAR search for '"' or '\\')
+    if (i + 4 <= len) {
+      const uint32_t x = get4(i), q = x ^ 0x22222222u, e = x ^ 0x5C5C5C5Cu;
+      const uint32_t m = ((q - 0x01010101u) & ~q & 0x80808080u) | ((e - 0x01010101u) & ~e & 0x80808080u);
+      if (!m) { i += 4; continue; }
+      i += (uint32_t)__builtin_ctz(m) >> 3;  // the lowest flagged byte is the first real match
+    } else if (i >= len) {
+      return false;
+    }
     const uint32_t c = byte(i);
     if (c == '"') break;
     if (c == '\\') return false;
+    i++;
   }
   const uint32_t nl = i - n0;
   i++;

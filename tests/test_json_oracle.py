@@ -74,3 +74,12 @@ def test_fast_path_taken_for_serializer_records_and_exact():
         assert json_cpu.fast_path(r)[0] is False
     for r in [c for c, _ in JC.CASES] + JC.fuzz(5, 5000):
         assert json_cpu.fast_path(r)[1], r
+
+
+def test_fast_path_name_lengths():
+    for n in range(0, 24):
+        for name in ("x" * n, "é" * (n // 2), "a" * n + '\\"', "\t" * n):
+            r = b'{"name":"%s","price":%d,"volume":%d}' % (name.encode(), n, -n)
+            fast, agree = json_cpu.fast_path(r)
+            assert agree, r
+            assert fast == ("\\" not in name), r
