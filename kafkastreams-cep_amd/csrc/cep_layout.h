@@ -21,6 +21,7 @@ constexpr int kMaxStates = 8;      // fold state names per query (MAXF)
 constexpr int kMaxAggs = 8;        // folds per pattern
 constexpr int kMaxStack = 16;      // interpreter stack depth
 constexpr int kDeweyPairs = 6;     // RLE pairs per Dewey version (overflow -> CEP_KEY_CAPACITY)
+constexpr int kMaxStencil = 8;     // stages of a CEP_KIND_STENCIL query (stencil.hip instantiations)
 
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
 enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3 };

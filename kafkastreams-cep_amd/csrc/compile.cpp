@@ -836,7 +836,9 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
 
   // CEP_KIND_STENCIL gate: every pattern ONE + STRICT, predicates total
   // and state-free (so evaluating them everywhere cannot throw or differ), distinct names.
-  bool stencil = np <= 32;
+  // The stencil kernels are instantiated for 1..kMaxStencil stages (stencil.hip
+  // launch_stencil); a longer strict chain runs on the NFA kernel.
+  bool stencil = np <= kMaxStencil;
   std::vector<int> seen;
   for (auto& p : ps) {
     if (p.card != CARD_ONE || p.strat != STRICT || !total(p.pred.get())) stencil = false;

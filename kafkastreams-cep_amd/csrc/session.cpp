@@ -204,14 +204,14 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const bool range = q->stencilRange;
   for (int c = 0; c < 2; c++) a.col[c] = (const int32_t*)s->cols.p[q->rangeCols[c]];
   a.aligned = ((uintptr_t)a.col[0] % 16 == 0) && ((uintptr_t)a.col[1] % 16 == 0);
-  for (uint32_t i = 0; i < m && i < 8; i++) {
+  for (uint32_t i = 0; i < m && i < (uint32_t)kMaxStencil; i++) {
     a.prog[i] = q->stencilProg[i];
     for (int c = 0; c < 2; c++) {
       a.rs[i].lo[c] = q->rangeLo[i][c];
       a.rs[i].hi[c] = q->rangeHi[i][c];
     }
   }
-  for (uint32_t x = 0; x < m && x < 8; x++) a.stage_name[x] = q->arityStage[x];
+  for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
   a.tile_cnt = s->tile_key.as<uint32_t>() + (n_tiles + 1);
   a.group_cnt = s->status.as<uint32_t>();
@@ -651,6 +651,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     return fail(CEP_E_INVALID, "null argument");
   if (b->n_keys >= 0xFFFFFFFFull || b->n_events >= 0xFFFFFFFFull)
     return fail(CEP_E_INVALID, "a batch holds < 2^32 keys and events (sequence numbers are u32)");
+  if (b->arrival_key && b->n_events >= 0x80000000ull)
+    return fail(CEP_E_INVALID, "an arrival-order batch holds < 2^31 events (split it)");
   return guarded([&] {
     DeviceGuard g(s->device);
     const cep_query* q0 = s->qs[0]->q;

@@ -22,8 +22,8 @@ struct StencilArgs {
   const uint32_t* code;
   Cols cols;
   const int64_t* ts;
-  uint16_t prog[8];
-  uint16_t stage_name[8];    // walk order: stage name of pair t (t = 0 is the final event)
+  uint16_t prog[kMaxStencil];
+  uint16_t stage_name[kMaxStencil];    // walk order: stage name of pair t (t = 0 is the final event)
   bool aligned;              // col[] 16-B aligned: vector loads
   // pass 1 -> pass 3
   uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k

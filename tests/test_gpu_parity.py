@@ -52,6 +52,21 @@ def test_cfg2_strict_abc_small(force_nfa, tier):
     assert_parity(gpu_run(ir, off, cols, force_nfa=force_nfa, tier=tier), oracle.run(ir, off, cols, threads=8), off)
 
 
+@pytest.mark.parametrize("n", [8, 9, 12])
+def test_long_strict_chain(n):
+    """a strict ONE-only chain of more than 8 stages compiles for the NFA kernel
+    (the stencil is instantiated for at most 8) and matches the oracle."""
+    from test_native_abi import strict_chain
+    rng = np.random.default_rng(n)
+    off = np.array([0, 3000, 3000, 7000], np.uint64)
+    v = (np.arange(7000) % 4).astype(np.int32)  # long runs of the chain's own pattern
+    v[rng.integers(0, 7000, size=300)] = rng.integers(0, 4, size=300)
+    ir = strict_chain(n).to_ir()
+    r = oracle.run(ir, off, [v])
+    assert r["n_matches"] > 100
+    assert_parity(gpu_run(ir, off, [v]), r, off)
+
+
 def test_stencil_many_short_keys():
     """More key starts than a 4096-event tile holds keys: the LDS boundary table path."""
     rng = np.random.default_rng(7)

@@ -42,6 +42,24 @@ def test_compile_kinds():
     assert s.kind == N.CEP_KIND_STENCIL and s.info.arity == 3
 
 
+def strict_chain(n):
+    """SEQ(S0..S{n-1}) all ONE + strict, S_i: v % 4 == i % 4 (total, state-free)."""
+    S = EventSchema({"v": "int"})
+    b = QueryBuilder(S)
+    for i in range(n):
+        sel = b.select(f"S{i}").where(lambda k, v, ts, s, i=i: v.v % 4 == i % 4)
+        b = sel.then() if i < n - 1 else sel
+    return b.build()
+
+
+@pytest.mark.parametrize("n,kind", [(8, N.CEP_KIND_STENCIL), (9, N.CEP_KIND_NFA), (12, N.CEP_KIND_NFA)])
+def test_stencil_gate_stage_limit(n, kind):
+    """The stencil kernels are instantiated for at most 8 stages: a longer strict chain is
+    compiled for the NFA kernel (it would otherwise fail at every push)."""
+    q = N.Query(strict_chain(n).to_ir())
+    assert q.kind == kind and q.info.n_patterns == n
+
+
 def _pred(k, v, ts, s):
     return v.price > 1
 
