@@ -572,6 +572,10 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   bool fold32 = true;  // every state a Java int: one word per fold slot in the run record
   for (uint32_t i = 0; i < d.n_states; i++) fold32 = fold32 && d.state_type[i] == 1;
   o += "  static constexpr bool kFold32 = " + std::string(fold32 ? "true" : "false") + ";\n";
+  // run-queue slots in LDS per half ($CEP_RING_LDS caps it, for measurement runs)
+  std::string rl = "ring_lds_slots<RecLayout<F, kFold32>>()";
+  if (const char* v = std::getenv("CEP_RING_LDS")) rl = "(" + rl + " < " + std::to_string(std::atoi(v)) + " ? " + rl + " : " + std::to_string(std::atoi(v)) + ")";
+  o += "  static constexpr uint32_t kRingLds = " + rl + ";\n";
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
   o += "  typedef Ev EvT;\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
@@ -715,7 +719,9 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   std::string occ;
   if (waves > 0) occ = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))";
   o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256)" + occ + " cep_nfa_jit(NfaArgs A) {\n";
-  o += "  JitQ q(A);\n  run_key<F>(A, q);\n}\n\n";
+  o += "  JitQ q(A);\n";
+  o += "  __shared__ v4u ring_lds[JitQ::kRingLds > 0 ? 4 * 2 * JitQ::kRingLds * RecLayout<F, JitQ::kFold32>::kLdsQuads * 64 : 1];\n";
+  o += "  run_key<F>(A, q, JitQ::kRingLds > 0 ? ring_lds : nullptr);\n}\n\n";
   if (bpred) {
     // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
     // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
@@ -731,6 +737,15 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
+    // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
+    // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).
+    o += "__device__ __forceinline__ bool begin_hit_at(const NfaArgs& A, uint64_t p) {\n";
+    o += "  Ev e;\n  ld_bev(e, A, p);\n  Fo f;\n  f.nm = (1u << F) - 1;\n  int err = 0;\n";
+    o += "  return " + predName[d.begin_stage][0] + "(e, f, err) || err;\n}\n";
+    o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_bits(NfaArgs A) {\n";
+    o += "  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n";
+    o += "  const uint64_t b = __ballot(p < A.n_events && begin_hit_at(A, p));\n";
+    o += "  if ((threadIdx.x & 63) == 0 && p < A.n_events) A.bhits[p >> 6] = b;\n}\n\n";
   }
   o += "}  // namespace cep\n";
   return o;

@@ -38,6 +38,9 @@ struct NfaArgs {
   KeyState* ks;
   KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
   uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)
+  uint64_t* bhits;           // cep_nfa_bits: bit p = the begin predicate (null folds) is true or
+                             // throws at CSR position p (quiet lanes jump to the next set bit)
+  uint64_t n_events;         // CSR positions of the batch (bits kernel)
   uint32_t* n_capacity_err;  // keys that hit CEP_KEY_CAPACITY
 };
 

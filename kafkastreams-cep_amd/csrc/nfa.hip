@@ -39,6 +39,7 @@ struct InterpQ {
   uint32_t begin_stage;
   static constexpr bool kBeginReg = false;  // quiet is only known at run time here
   static constexpr bool kFold32 = false;     // fold slots hold any state type
+  static constexpr uint32_t kRingLds = 0;    // LDS holds the DevQuery and bytecode: queues in HBM
   struct EvT {};                             // the programs read the columns themselves
 
   __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {

@@ -36,6 +36,15 @@
 // written with ev_first = kPending and resolved when it is next loaded (event j+1, or the
 // final-match pass of event j itself).
 //
+// LDS slots (Q::kRingLds = RL > 0).  The first RL slots of each half live in LDS instead of
+// HBM: their header quad, first Dewey quad and fold quads (the quads every record uses); the
+// remaining Dewey quads (pairs 2.., rare) stay at the slot's HBM position.  A lane whose queue
+// holds at most RL records between events - most lanes at most events - then never touches
+// HBM for its run queue.  The slot index of the queue loop is wave-uniform (lanes iterate
+// i = 0, 1, ... in lockstep), so the LDS/HBM choice does not diverge there.  LDS is per
+// launch: a streaming session spills the LDS slots of a key's queue to their HBM positions
+// when the batch ends and reloads them when the next batch starts.
+//
 // When the begin stage has a single BEGIN edge (kBeginReg) the begin run, always the last
 // record of the queue (NFA.java:148-157 re-adds it after its own outputs), lives in
 // registers as its single Dewey digit: the ring holds live runs only.
@@ -75,6 +84,13 @@ constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
 // may_alias: quads of Node/Pred are also read and written field by field (Node::refs, ...);
 // without it TBAA lets the compiler reorder the two views of the same bytes
 typedef uint32_t v4u __attribute__((ext_vector_type(4), may_alias));
+// LDS-typed quads: a load from LDS and one from HBM of the same shape in the two arms of a
+// branch must not be merged into one flat load through a pointer select (the compiler
+// would otherwise do exactly that); distinct address spaces cannot be merged.
+#ifndef CEP_LDS_AS
+#define CEP_LDS_AS __attribute__((address_space(3)))
+#endif
+typedef CEP_LDS_AS v4u lds_v4u;
 
 // W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
 template <int F, bool W32 = false>
@@ -82,7 +98,18 @@ struct RecLayout {
   static constexpr int kDwQuads = (kDeweyPairs + 1) / 2;
   static constexpr int kFoldQuads = W32 ? (1 + F + 3) / 4 : (2 + 2 * F + 3) / 4;
   static constexpr int kQuads = 1 + kDwQuads + kFoldQuads;
+  // quads of an LDS slot: header, Dewey quad 0, folds
+  static constexpr int kLdsQuads = 2 + kFoldQuads;
+  __host__ __device__ static constexpr bool in_lds(int quad) { return quad <= 1 || quad > kDwQuads; }
+  __host__ __device__ static constexpr int lds_quad(int quad) { return quad <= 1 ? quad : quad - (kDwQuads - 1); }
 };
+
+// LDS slots per queue half for a record layout: 192 B of LDS per lane (48 KiB per 256-lane
+// block keeps 3 blocks = 3 waves per SIMD resident), at most 2 slots
+template <class Lay>
+__host__ __device__ constexpr int ring_lds_slots() {
+  return (192 / (2 * 16 * Lay::kLdsQuads)) < 2 ? (192 / (2 * 16 * Lay::kLdsQuads)) : 2;
+}
 
 // bytes of double-buffered run queues for n_slots lanes of rcap records (64-bit folds: the
 // larger layout, so one allocation serves every query)
@@ -101,6 +128,7 @@ struct Lane {
   using Lay = RecLayout<F, Q::kFold32>;
   using EvT = typename Q::EvT;
   static constexpr bool kBeginReg = Q::kBeginReg;
+  static constexpr uint32_t kRL = Q::kRingLds;  // LDS slots per half (0: all HBM)
   const NfaArgs& A;
   Q& q;
   uint32_t key;
@@ -111,6 +139,7 @@ struct Lane {
   EvT ev;             // fields of event ev_pos
   uint32_t ev_pos = CEP_NONE;
   v4u* rb;  // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
+  lds_v4u* lr;  // LDS slots: this lane's quad 0 of half 0, slot 0 (stride 64 quads)
   v4u* wb;  // this lane's walk queue, slot 0 quad 0 (stride 64 quads)
   uint32_t half = 0, count = 0, ocount = 0;  // input half, its records, records written
   uint32_t bdig = 1;                         // kBeginReg: the begin run's version "bdig"
@@ -134,11 +163,37 @@ struct Lane {
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
   }
+  __device__ __forceinline__ lds_v4u* LQ(uint32_t h, uint32_t slot, int lq) const {
+    return lr + ((h * kRL + slot) * Lay::kLdsQuads + lq) * 64;
+  }
+  // quad `quad` (compile-time) of a queue slot, from LDS or HBM
+  __device__ __forceinline__ bool lds_slot(uint32_t slot, int quad) const {
+    return kRL > 0 && Lay::in_lds(quad) && slot < kRL;
+  }
+  __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad) const {
+    if (lds_slot(slot, quad)) return *LQ(h, slot, Lay::lds_quad(quad));
+    return *QP(h, slot, quad);
+  }
+  __device__ __forceinline__ void wr(uint32_t h, uint32_t slot, int quad, const v4u& v) const {
+    if (lds_slot(slot, quad)) *LQ(h, slot, Lay::lds_quad(quad)) = v;
+    else *QP(h, slot, quad) = v;
+  }
+  // streaming: the LDS slots of the queue (half `half`, `count` records) <-> their HBM positions
+  __device__ __forceinline__ void lds_spill(bool to_hbm) {
+    for (uint32_t s = 0; s < kRL && s < count; s++) {
+#pragma unroll
+      for (int k = 0; k < Lay::kQuads; k++)
+        if (Lay::in_lds(k)) {
+          if (to_hbm) *QP(half, s, k) = *LQ(half, s, Lay::lds_quad(k));
+          else *LQ(half, s, Lay::lds_quad(k)) = *QP(half, s, k);
+        }
+    }
+  }
 
   // ---------------------------------------------------------------- records
   // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
   __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf) const {
-    const v4u hd = *QP(h, slot, 0);
+    const v4u hd = rd(h, slot, 0);
     r.stage = hd.x & 0x00FFFFFFu;
     r.event = hd.y;
     r.ev_first = hd.z == kPending ? pf : hd.z;
@@ -147,7 +202,7 @@ struct Lane {
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++) {
       v4u d = {0, 0, 0, 0};
-      if ((uint32_t)(2 * k) < r.ver.n) d = *QP(h, slot, 1 + k);
+      if ((uint32_t)(2 * k) < r.ver.n) d = rd(h, slot, 1 + k);
       r.ver.v[2 * k] = (int32_t)d.x;
       r.ver.c[2 * k] = d.y;
       if (2 * k + 1 < kDeweyPairs) {
@@ -158,7 +213,7 @@ struct Lane {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++) {
-      const v4u d = *QP(h, slot, 1 + Lay::kDwQuads + k);
+      const v4u d = rd(h, slot, 1 + Lay::kDwQuads + k);
       w[4 * k] = d.x;
       w[4 * k + 1] = d.y;
       w[4 * k + 2] = d.z;
@@ -173,13 +228,13 @@ struct Lane {
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
                                              uint32_t ev_first, const Dewey& ver0) {
     const Dewey ver = dw_pin(ver0);
-    *QP(h, slot, 0) = v4u{stage | (ver.n << 24), event, ev_first, ver.len};
+    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, ver.len});
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
-        *QP(h, slot, 1 + k) = v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
-                                  2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
-                                  2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u};
+        wr(h, slot, 1 + k, v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
+                               2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
+                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u});
   }
 
   __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm) {
@@ -198,12 +253,12 @@ struct Lane {
     }
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++)
-      *QP(h, slot, 1 + Lay::kDwQuads + k) = v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]});
   }
 
   __device__ __forceinline__ void copy_rec(uint32_t h, uint32_t from, uint32_t to) {
 #pragma unroll
-    for (int k = 0; k < Lay::kQuads; k++) *QP(h, to, k) = *QP(h, from, k);
+    for (int k = 0; k < Lay::kQuads; k++) wr(h, to, k, rd(h, from, k));
   }
 
   // Appends an output record (header + version) and returns its slot, -1 when the queue is
@@ -623,7 +678,7 @@ struct Lane {
     // matchConstruction: finals in order, then drop them from the queue
     uint32_t w = 0;
     for (uint32_t i = 0; i < count; i++) {
-      const v4u hd = *QP(oh, i, 0);
+      const v4u hd = rd(oh, i, 0);
       if (hd.x & kRecFinal) {
         Rec<F> r;
         load(oh, i, r, cur_first);
@@ -646,7 +701,7 @@ struct Lane {
   __device__ __forceinline__ bool only_begin() const {
     if (kBeginReg) return count == 0;
     if (count != 1) return false;
-    return ((*QP(half, 0, 0)).x & 0x00FFFFFFu) == q.begin_stage;
+    return (rd(half, 0, 0).x & 0x00FFFFFFu) == q.begin_stage;
   }
 
   __device__ __forceinline__ void run() {
@@ -660,7 +715,27 @@ struct Lane {
         if (err) break;
       }
       bool known = false;
-      if (q.quiet && only_begin()) {
+      if (q.quiet && A.bhits && only_begin()) {
+        // the next event whose begin predicate holds or throws, 64 positions per word;
+        // event() evaluates the predicate there itself (its exception, in order)
+        uint64_t p = base + jj;
+        uint64_t w = A.bhits[p >> 6] >> (p & 63);
+        while (!w) {
+          jj += 64 - (uint32_t)(p & 63);
+          if (jj >= n) break;
+          p = base + jj;
+          w = A.bhits[p >> 6];
+        }
+        if (jj >= n) {
+          jj = n;
+          continue;
+        }
+        jj += (uint32_t)__builtin_ctzll(w);
+        if (jj >= n) {
+          jj = n;
+          continue;
+        }
+      } else if (q.quiet && only_begin()) {
         const uint32_t lim = (n - jj > kQuietChunk) ? jj + kQuietChunk : n;
         const uint32_t h = q.begin_scan(*this, jj, lim);
         if (err) {
@@ -702,7 +777,7 @@ struct Lane {
 // Driver shared by the AOT and JIT kernels: slot -> key, initial or carried state, the
 // batch's events of the key, KeyState (and KeyCarry for the next batch of a stream).
 template <int F, class Q>
-__device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
+__device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullptr) {
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nslots = A.key_list ? A.n_list : A.n_keys;
   if (slot >= nslots) return;
@@ -713,6 +788,8 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
   L.rb = reinterpret_cast<v4u*>(A.rings) +
          (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (slot % 64);
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
+  if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
+    L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);
   KeyState& ks = A.ks[key];
   KeyCarry* kc = A.carry ? A.carry + key : nullptr;
   if (kc && kc->live) {  // the key's NFA as the previous batch left it
@@ -733,6 +810,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
     L.pcur = kc->pcur;
     L.pend = kc->pend;
     L.opc = kc->opc;
+    L.lds_spill(false);  // the queue's first slots back into LDS
   } else {
     // NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1
     L.bdig = 1;
@@ -757,6 +835,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q) {
   ks.err_seq = L.err_seq;
   if (L.err == KE_CAPACITY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
   if (kc) {
+    if (!L.err) L.lds_spill(true);  // LDS ends with the launch: the queue continues from HBM
     kc->live = 1;
     kc->seq = L.j0 + L.n_ev;
     kc->half = L.half;

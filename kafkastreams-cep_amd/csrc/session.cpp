@@ -94,6 +94,7 @@ struct QueryRt {
   hipModule_t mod = nullptr;  // JIT tier: the query's own nfa kernel (cep_nfa_jit)
   hipFunction_t fn = nullptr;
   hipFunction_t fn_est = nullptr;  // cep_nfa_est (queries whose begin stage has one BEGIN edge)
+  hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
   double jit_compile_s = 0;
   DBuf est, order, order_tmp, est_sorted;
   void* sort_tmp = nullptr;  // hipCUB scratch of the lane-order sort
@@ -146,7 +147,7 @@ struct cep_session {
   std::vector<uint32_t> h_perm;
   bool layout_host_valid = false;
   // scratch
-  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask;
+  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask, bhits;
 };
 
 namespace {
@@ -367,6 +368,15 @@ void run_nfa(cep_session* s, QueryRt& r) {
     a.key_list = r.order.as<uint32_t>();
     a.n_list = (uint32_t)nk;
   }
+  a.n_events = s->n_events;
+  if (r.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
+    s->bhits.ensure(8 * ((s->n_events + 63) / 64));
+    a.bhits = s->bhits.as<uint64_t>();
+    size_t size = sizeof(NfaArgs);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    HIPCHECK(hipModuleLaunchKernel(r.fn_bits, (uint32_t)((s->n_events + 255) / 256), 1, 1, 256, 1, 1, 0, s->stream,
+                                   nullptr, cfg));
+  }
   HIPCHECK(launch_nfa_tier(r, a, nk, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   r.launches++;
@@ -562,8 +572,10 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         std::vector<char> co = jit_code_object(queries[i]->jitSource, &r->jit_compile_s);
         HIPCHECK(hipModuleLoadData(&r->mod, co.data()));
         HIPCHECK(hipModuleGetFunction(&r->fn, r->mod, "cep_nfa_jit"));
-        if (queries[i]->jitSource.find("cep_nfa_est") != std::string::npos)  // (a failed lookup would stick)
+        if (queries[i]->jitSource.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
           HIPCHECK(hipModuleGetFunction(&r->fn_est, r->mod, "cep_nfa_est"));
+          HIPCHECK(hipModuleGetFunction(&r->fn_bits, r->mod, "cep_nfa_bits"));
+        }
       }
       s->qs.push_back(std::move(r));
     }

@@ -1,0 +1,74 @@
+"""NFA kernel variants on the bench workload (cfg 3 stream in HBM), selected by the JIT
+generator's measurement knobs ($CEP_RING_LDS, $CEP_JIT_WAVES, $CEP_WALK_FLUSH, ...), each a
+separately generated kernel.  Prints kernel ms and the checksum per variant (the checksums
+must agree).  --precompile fills the JIT cache for every variant (no GPU needed).
+    python profiles/nfa_env_sweep.py [--keys N] [--variants name=K:V,K:V;...] [--precompile]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import cepamd  # noqa: E402,F401
+from kafkastreams_cep_amd import native as N  # noqa: E402
+from kafkastreams_cep_amd import workloads as W  # noqa: E402
+
+KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK")
+DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
+
+
+def parse(spec):
+    out = []
+    for item in spec.split(";"):
+        name, _, kv = item.partition("=")
+        env = dict(x.split(":") for x in kv.split(",") if x)
+        out.append((name, env))
+    return out
+
+
+def query(name, env, variant):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    q = N.Query(W.stock_query(variant).to_ir() if variant != "any" else W.any_kleene_query().to_ir())
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    return q
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--keys", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--query", default="readme")
+    ap.add_argument("--variants", default=DEFAULT)
+    ap.add_argument("--precompile", action="store_true")
+    args = ap.parse_args()
+    vs = parse(args.variants)
+    if args.precompile:
+        for name, env in vs:
+            print(name, query(name, env, args.query).precompile())
+        return
+    cfg = W.CONFIGS[3]
+    stream = N.synth_stream("stock", cfg.seed, args.keys, cfg.mean_events)
+    res = {}
+    for name, env in vs:
+        s = N.Session(query(name, env, args.query))
+        s.push_device(stream)
+        ks = []
+        for _ in range(args.steps):
+            s.push_device(stream)
+            ks.append(s.timing(0)[0])
+        n, d = s.digest(0)
+        code, _ = s.key_errors(0)
+        res[name] = {"kernel_ms": min(ks), "all_ms": ks, "matches": n, "checksum": f"{d:016x}",
+                     "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2]}
+        print(name, json.dumps(res[name]), flush=True)
+        s.close()
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

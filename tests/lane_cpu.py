@@ -51,7 +51,7 @@ def build(ir: bytes):
         os.replace(tmp, so)
     lib = C.CDLL(so)
     lib.lane_run.argtypes = [C.c_uint64, C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_void_p,
-                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_int]
+                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int]
     lib.lane_n_matches.restype = C.c_uint64
     lib.lane_n_pairs.restype = C.c_uint64
     lib.lane_fetch.argtypes = [C.c_void_p] * 7
@@ -59,9 +59,10 @@ def build(ir: bytes):
     return lib
 
 
-def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True):
+def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True):
     """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
-    the batch continues the keys' streams of the previous streaming call (reset=False)."""
+    the batch continues the keys' streams of the previous streaming call (reset=False).
+    bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the chunked scan."""
     lib = build(ir)
     if streaming and reset:
         lib.lane_stream_reset()
@@ -71,7 +72,7 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True):
     nk = len(key_off) - 1
     retried = C.c_uint32()
     lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried),
-                 1 if streaming else 0)
+                 1 if streaming else 0, 1 if bits else 0)
     nm, npairs = lib.lane_n_matches(), lib.lane_n_pairs()
     key = np.zeros(nm, np.uint32)
     emit = np.zeros(nm, np.uint32)
@@ -83,7 +84,7 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True):
     lib.lane_fetch(*[a.ctypes.data for a in (key, emit, off, seq, stage, err, err_seq)])
     m = {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
          "pair_seq": seq, "pair_stage": stage, "err_code": err, "err_seq": err_seq,
-         "retried": retried.value}
+         "retried": retried.value, "bits_used": bool(lib.lane_bits_used())}
     m["emit_pos"] = (key_off[key.astype(np.int64)] + emit).astype(np.uint64)
     pk = np.repeat(key.astype(np.int64), np.diff(off.astype(np.int64)))
     m["pair_pos"] = (key_off[pk] + seq).astype(np.uint64)

@@ -37,11 +37,25 @@ struct Stream {
   uint32_t node_top = 0, pred_top = 0;
 };
 static Stream g_stream;
+static bool g_bits_used = false;
+extern "C" int lane_bits_used() { return g_bits_used; }
 
 extern "C" void lane_stream_reset() { g_stream = Stream{}; }
 
+// the begin-hit bitmap (cep_nfa_bits), one position at a time; absent when the query's begin
+// stage is not a single BEGIN edge (no bits kernel)
+template <class A_>
+static auto fill_bits(const A_& a, std::vector<uint64_t>& bits, int) -> decltype(begin_hit_at(a, 0), bool()) {
+  for (uint64_t p = 0; p < a.n_events; p++)
+    if (begin_hit_at(a, p)) bits[p >> 6] |= 1ull << (p & 63);
+  return true;
+}
+template <class A_>
+static bool fill_bits(const A_&, std::vector<uint64_t>&, long) { return false; }
+
 extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const* cols, int n_cols,
-                        const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried, int streaming) {
+                        const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried, int streaming,
+                        int use_bits) {
   using namespace cep;
   signal(SIGSEGV, on_fault);
   const uint64_t ne = key_off[nk];
@@ -92,6 +106,10 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   a.out_pool = Pool{&out_top, (uint32_t)(out.size() / kOutChunkWords), 1};
   a.ks = ks.data();
   a.n_capacity_err = &n_cap;
+  a.n_events = ne;
+  std::vector<uint64_t> bits((ne + 63) / 64 + 1, 0);
+  g_bits_used = use_bits && fill_bits(a, bits, 0);
+  if (g_bits_used) a.bhits = bits.data();
   auto launch = [&](uint64_t nslots, uint32_t rc, int df) {
     std::vector<v4u> rings_batch;
     if (!streaming) {

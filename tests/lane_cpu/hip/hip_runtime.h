@@ -11,6 +11,8 @@
 #define __global__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
+#define __shared__ static  // one lane at a time: the block's LDS is one static array
+#define CEP_LDS_AS           // (no address spaces on the host)
 #define asm(...) ((void)0)
 
 struct LaneDim3 {
@@ -24,6 +26,7 @@ inline unsigned atomicAdd(unsigned* p, unsigned v) {
   return o;
 }
 inline bool __any(int x) { return x != 0; }  // a wave of one lane
+inline unsigned long long __ballot(int x) { return x != 0; }  // (cep_nfa_bits: built, not run)
 inline double __longlong_as_double(long long x) {
   double d;
   std::memcpy(&d, &x, 8);

@@ -25,7 +25,8 @@ def _irs(bench_only):
     for name, case in kats().items():
         if name in STRING_KATS:
             irs.append(build_case(name, case)[0].to_ir())
-    irs += [random_query(s).to_ir() for s in range(0, 160)]
+    from test_gpu_parity import FUZZ_JIT_SEEDS  # the interpreter-tier seeds need no JIT kernel
+    irs += [random_query(s).to_ir() for s in FUZZ_JIT_SEEDS]
     return irs
 
 
@@ -42,9 +43,19 @@ def _compile(ir):
 def main(bench_only=False, workers=None):
     irs = _irs(bench_only)
     t = time.time()
+    os.environ["CEP_JIT_TOUCH"] = "1"  # cache hits refresh their entry's mtime (jit.cpp)
     with ProcessPoolExecutor(workers or min(8, os.cpu_count() or 1)) as ex:
         spent = list(ex.map(_compile, irs))
-    print(f"jit cache: {len(irs)} queries, {sum(1 for s in spent if s > 0)} compiled, {time.time() - t:.1f}s")
+    pruned = 0
+    if not bench_only:  # entries no current query maps to (an older kernel source): dropped
+        cache = os.path.join(ROOT, "kafkastreams-cep_amd", "jit_cache")
+        for f in os.listdir(cache) if os.path.isdir(cache) else []:
+            p = os.path.join(cache, f)
+            if f.endswith(".co") and os.path.getmtime(p) < t - 1:
+                os.remove(p)
+                pruned += 1
+    print(f"jit cache: {len(irs)} queries, {sum(1 for s in spent if s > 0)} compiled, {pruned} stale entries "
+          f"dropped, {time.time() - t:.1f}s")
 
 
 if __name__ == "__main__":

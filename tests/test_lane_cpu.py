@@ -30,7 +30,10 @@ def test_lane_stock_small(variant):
     ir = W.stock_query(variant).to_ir()
     r = oracle.run(ir, off, cols, threads=8)
     assert r["n_matches"] > 20
-    lane_cpu.assert_same(lane_cpu.run(ir, off, cols), r, off)
+    g = lane_cpu.run(ir, off, cols)
+    assert g["bits_used"]
+    lane_cpu.assert_same(g, r, off)
+    lane_cpu.assert_same(lane_cpu.run(ir, off, cols, bits=False), r, off)  # the chunked quiet scan
 
 
 def test_lane_any_kleene_small():
