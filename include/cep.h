@@ -111,6 +111,16 @@ const char* cep_query_jit_source(const cep_query* q);
 /* Compile the query's JIT kernel into the on-disk code-object cache without a GPU
  * ($CEP_JIT_CACHE, default <libcep.so dir>/jit_cache); sessions then load it directly. */
 int cep_jit_precompile(const cep_query* q, double* compile_s);
+/* The same for the kernel groups a session over these queries would launch (cep_opts.no_groups
+ * = 0): one code object per group of queries that differ only in literals. */
+int cep_jit_precompile_group(const cep_query* const* queries, int n_queries, double* compile_s);
+/* Kernel group `group` of a session over these queries: its members (query indices), the
+ * generated source and the per-query literal table (members x n_literals, row-major).  Arrays
+ * are owned by the library until the next call on this thread.  CEP_E_INVALID past the last
+ * group.  (Introspection: which queries share a launch, and what it compiles.) */
+int cep_query_group_plan(const cep_query* const* queries, int n_queries, int group, const char** source,
+                         uint32_t* n_members, const int32_t** members, uint32_t* n_literals,
+                         const int64_t** literals);
 
 #define CEP_TIER_JIT 0     /* NFA queries run their own kernel, generated and compiled by hipRTC */
 #define CEP_TIER_INTERP 1  /* NFA queries run the precompiled bytecode-interpreter kernel */
@@ -125,6 +135,10 @@ typedef struct {
                              events in consecutive batches are one stream, sequence numbers
                              continue; every batch has the same n_keys); 0: every batch starts
                              every key from the initial state */
+  int no_groups;          /* 1: every NFA query runs its own launch.  0 (default): in a per-batch
+                             JIT session, queries that differ only in literal values (config 5's
+                             64 variants) run as one kernel launch, lanes = (query, key), reading
+                             the batch's columns once for all of them */
 } cep_opts;
 
 int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts,
@@ -223,6 +237,20 @@ int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size);
 int cep_session_restore(cep_session* s, const void* buf, size_t size);
 
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);
+
+/* Where the last batch's NFA work went, for query `query`'s kernel group (queries sharing a
+ * launch report the same group figures; stencil queries report zeros but kernel_ms). */
+typedef struct {
+  uint32_t group;          /* kernel group of the query (-1 as u32: stencil) */
+  uint32_t group_queries;  /* queries in that launch */
+  double kernel_ms;        /* bitmap + lane order + matching launch + re-runs */
+  double main_ms;          /* the matching launch (cep_nfa_jit / nfa_kernel) alone */
+  double retry_ms;         /* re-runs of jobs that hit a capacity limit or a walk conflict */
+  uint64_t retried_jobs;   /* (query, key) jobs re-run */
+  uint64_t nodes_used, preds_used, out_chunks_used;  /* buffer pools at the end of the batch */
+  uint32_t launches;
+} cep_batch_stats;
+int cep_last_stats(cep_session* s, int query, cep_batch_stats* out);
 
 const char* cep_last_error(void);
 int cep_alloc_pinned(size_t bytes, void** out);

@@ -3,11 +3,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/cep.h"
 #include "cep_layout.h"
+
+namespace cep {
+struct ParsedQuery;
+}
 
 struct cep_query {
   cep_query_info info{};
@@ -22,11 +27,21 @@ struct cep_query {
   int nRangeCols = 0;
   int64_t rangeLo[8][2]{}, rangeHi[8][2]{};
   std::string jitSource;  // per-query NFA step policy for hipRTC (jit.cpp)
+  std::shared_ptr<cep::ParsedQuery> parsed;  // the parsed chain and stage build (plan_groups)
 };
 
 namespace cep {
 
 void compile_query(const uint8_t* ir, size_t n, cep_query* q);
+
+// queries sharing one kernel launch (compile.cpp plan_groups)
+struct GroupPlan {
+  std::vector<int> members;    // query indices, in session order
+  std::string source;          // the group's JIT source
+  uint32_t nkc = 0;            // literals per query in `table` (0: all compiled in)
+  std::vector<int64_t> table;  // members.size() x nkc
+};
+std::vector<GroupPlan> plan_groups(const std::vector<const cep_query*>& qs);
 
 struct NfaArgs;
 struct StencilArgs;
@@ -35,6 +50,8 @@ struct KeyState;
 hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap);  // double-buffered run queues
 uint64_t walkq_size(uint64_t n_slots, uint32_t wcap);        // deferred-walk queues
+hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list, uint32_t* conf_list,
+                                uint32_t* counts, hipStream_t st);
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,

@@ -26,8 +26,13 @@ constexpr int kMaxStencil = 8;     // stages of a CEP_KIND_STENCIL query (stenci
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
 enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3 };
 // KE_CONFLICT: a deferred walk would have changed what the step saw (nfa_lane.h); internal,
-// the key is re-run with walks in place
-enum KeyErr : int32_t { KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16, KE_CONFLICT = 17 };
+// the key is re-run with walks in place.  KE_RETRY: a resource of the launch ran out (run
+// queue, walk queue, node / predecessor / output pool); internal, the key is re-run with more.
+// KE_CAPACITY: a hard limit (Dewey RLE pairs, stage depth): final.  A KE_RETRY left after the
+// last re-run is reported as KE_CAPACITY.
+enum KeyErr : int32_t {
+  KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16, KE_CONFLICT = 17, KE_RETRY = 18
+};
 
 constexpr uint16_t kProgTrue = 0xFFFF;
 

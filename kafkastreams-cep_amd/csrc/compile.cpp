@@ -311,6 +311,12 @@ struct Builder {
 };
 
 
+// a compiled query's parse and stage build, kept for plan_groups
+struct ParsedQuery {
+  std::vector<PatternIR> ps;
+  std::unique_ptr<Builder> b;
+};
+
 // ============================================================ JIT source generation
 // Emits the per-query step policy compiled by hipRTC (jit.cpp): fields loaded once per
 // event into registers, predicates and folds as straight-line Java-semantics code, and one
@@ -336,9 +342,20 @@ std::string lit(const Expr* e) {
   return b;
 }
 
+// Literals of a query's predicates and folds, in generation order.  A group of queries that
+// differ only in literal values (config 5's 64 stock-query variants) shares one kernel: every
+// literal whose value differs across the group is read from a per-query constant table
+// (K.c[i], loaded once per lane) instead of being compiled in.
+struct LitCtx {
+  bool param = false;                // literals may come from the table
+  const std::vector<char>* inl = nullptr;  // param: literal i stays inline where inl[i] (null: none)
+  std::vector<int64_t> values;       // every literal's bits (int, long, double bits, bool)
+};
+
 struct Gen {
   std::string s;
   int n = 0;
+  LitCtx* L = nullptr;
   std::string fail;   // statement tail after `err = X;` (e.g. "return false;")
   int aggType = 0;    // state type of `curr` inside an aggregator
   std::string t() { return "t" + std::to_string(n++); }
@@ -347,7 +364,20 @@ struct Gen {
   // returns (value, null-flag or "")
   std::pair<std::string, std::string> expr(const Expr* e) {
     switch (e->op) {
-      case 0x01: case 0x02: case 0x03: case 0x04: return {lit(e), ""};
+      case 0x01: case 0x02: case 0x03: case 0x04: {
+        const size_t i = L->values.size();
+        int64_t bits = e->i;
+        if (e->op == 0x03) std::memcpy(&bits, &e->d, 8);
+        L->values.push_back(bits);
+        if (!L->param || (L->inl && (*L->inl)[i])) return {lit(e), ""};
+        const std::string k = "K.c[" + std::to_string(i) + "]";
+        switch (e->op) {
+          case 0x01: return {"((int32_t)" + k + ")", ""};
+          case 0x02: return {"((int64_t)" + k + ")", ""};
+          case 0x03: return {"__longlong_as_double(" + k + ")", ""};
+          default: return {"(" + k + " != 0)", ""};
+        }
+      }
       case 0x05: return {"ev.f" + std::to_string(e->idx), ""};
       case 0x06: return {"ev.ts", ""};
       case 0x07: case 0x08: {
@@ -487,7 +517,7 @@ void usesM(const M* m, std::vector<bool>& fields, bool& ts) {
 
 }  // namespace
 
-static std::string generate_jit(cep_query* q, Builder& b) {
+static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& lits) {
   const DevQuery& d = q->dev;
   const int F = d.n_states <= 2 ? 2 : d.n_states <= 4 ? 4 : 8;
   std::vector<int> stTypes(d.state_type, d.state_type + d.n_states);
@@ -531,16 +561,19 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   loader("ld_bev", bfields, bts);
   o += "\n";
   // predicates, one per (stage, edge); folds one per (stage, aggregate)
+  std::string pa;
   std::vector<std::vector<std::string>> predName(d.n_stages, std::vector<std::string>(3));
   for (auto& pe : b.pending) {
     if (pe.m->k == M::TRUE_) { predName[pe.stage][pe.edge] = ""; continue; }
     Gen g;
+    g.L = &lits;
     g.stateType = stTypes;
     g.fail = "return false;";
     const std::string v = g.matcher(pe.m.get());
     const std::string name = "P" + std::to_string(pe.stage) + "_" + std::to_string(pe.edge);
     predName[pe.stage][pe.edge] = name;
-    o += "__device__ __forceinline__ bool " + name + "(const Ev& ev, const Fo& w, int& err) {\n" + g.s + "  return " + v + ";\n}\n";
+    pa += "__device__ __forceinline__ bool " + name + "(const Ev& ev, const Fo& w, int& err, const Kc& K) {\n" + g.s +
+          "  (void)K;\n  return " + v + ";\n}\n";
   }
   std::vector<std::vector<std::string>> aggName(d.n_stages);
   for (auto& sa : b.stageAggs) {
@@ -548,6 +581,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     for (auto& a : *sa.second) {
       const int st = stTypes[a.first];
       Gen g;
+      g.L = &lits;
       g.stateType = stTypes;
       g.fail = "return;";
       g.aggType = st;
@@ -560,11 +594,19 @@ static std::string generate_jit(cep_query* q, Builder& b) {
       aggName[sa.first].push_back(name);
       std::string store = st == 3 ? "__double_as_longlong(" + r.first + ")" : "(int64_t)" + r.first;
       std::string nul = r.second.empty() ? "0u" : "(" + r.second + " ? 1u : 0u)";
-      o += "__device__ __forceinline__ void " + name + "(const Ev& ev, Fo& w, int& err) {\n" + head + g.s +
-           "  w.v[" + si + "] = " + store + ";\n  w.nm = (w.nm & ~(1u << " + si + ")) | (" + nul + " << " + si + ");\n}\n";
+      pa += "__device__ __forceinline__ void " + name + "(const Ev& ev, Fo& w, int& err, const Kc& K) {\n" + head +
+            g.s + "  (void)K;\n  w.v[" + si + "] = " + store + ";\n  w.nm = (w.nm & ~(1u << " + si + ")) | (" + nul +
+            " << " + si + ");\n}\n";
     }
   }
-  o += "\nstruct JitQ {\n  const NfaArgs& A;\n";
+  // the per-query constant table (parametric literals), then the predicates and folds
+  const size_t nkc = lits.param ? lits.values.size() : 0;
+  o += "constexpr int NKC = " + std::to_string(nkc) + ";  // literals per query in NfaArgs.kc\n";
+  o += "struct Kc {\n  int64_t c[NKC > 0 ? NKC : 1];\n};\n";
+  o += "__device__ __forceinline__ void ld_kc(Kc& K, const NfaArgs& A, uint32_t qi) {\n";
+  o += "  for (int i = 0; i < NKC; i++) K.c[i] = A.kc[(uint64_t)qi * NKC + i];\n  (void)K; (void)A; (void)qi;\n}\n";
+  o += pa;
+  o += "\nstruct JitQ {\n  const NfaArgs& A;\n  Kc K;  // this lane's query constants (group kernels)\n";
   const DevStage& bs = d.st[d.begin_stage];
   const bool quiet = bs.n_edges == 1 && bs.e[0].op == OP_BEGIN;
   o += "  static constexpr bool quiet = " + std::string(quiet ? "true" : "false") + ";\n";
@@ -579,6 +621,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
   o += "  typedef Ev EvT;\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
+  o += "  __device__ __forceinline__ void set_query(uint32_t qi) { ld_kc(K, A, qi); }\n";
   o += "  __device__ __forceinline__ void load_ev(Ev& e, uint64_t pos) const { ld_ev(e, A, pos); }\n";
   o += "  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {\n    if (sw & kRecEps) return (sw >> 8) & 0xFF;\n    switch (sw & 0xFF) {\n";
   for (uint32_t s = 0; s < d.n_stages; s++) o += "      case " + std::to_string(s) + ": return " + std::to_string(d.st[s].sk) + ";\n";
@@ -590,7 +633,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
   const bool bpred = quiet && !predName[d.begin_stage][0].empty();
   if (bpred) {
     o += "    Fo w;\n    w.nm = (1u << F) - 1;\n    int err = 0;\n";
-    o += "    const bool r = " + predName[d.begin_stage][0] + "(L.ev, w, err);\n    if (err) L.err = err;\n    return r;\n";
+    o += "    const bool r = " + predName[d.begin_stage][0] + "(L.ev, w, err, K);\n    if (err) L.err = err;\n    return r;\n";
   } else {
     o += "    return true;\n";
   }
@@ -603,7 +646,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     o += "#pragma unroll\n    for (uint32_t i = 0; i < kQuietChunk; i++) ld_bev(e[i], A, L.base + (j0 + i < lim ? j0 + i : j0));\n";
     o += "#pragma unroll\n    for (uint32_t i = 0; i < kQuietChunk; i++) {\n      if (j0 + i >= lim) break;\n";
     o += "      Fo w;\n      w.nm = (1u << F) - 1;\n      int err = 0;\n";
-    o += "      const bool r = " + predName[d.begin_stage][0] + "(e[i], w, err);\n";
+    o += "      const bool r = " + predName[d.begin_stage][0] + "(e[i], w, err, K);\n";
     o += "      if (err) { L.err = err; return j0 + i; }\n      if (r) return j0 + i;\n    }\n    return lim;\n";
   } else {
     o += "    return j0;\n";
@@ -621,7 +664,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     f += "    int err = 0;\n";
     for (int e = 0; e < S.n_edges; e++) {  // matchEdgesAndGet: every predicate first, in order
       const std::string& pn = predName[s][e];
-      f += "    const bool m" + std::to_string(e) + " = " + (pn.empty() ? std::string("true") : pn + "(ev, w, err)") + ";\n";
+      f += "    const bool m" + std::to_string(e) + " = " + (pn.empty() ? std::string("true") : pn + "(ev, w, err, K)") + ";\n";
       if (!pn.empty()) f += "    if (err) { L.err = err; return; }\n";
     }
     std::string hasT = "false", hasP = "false", hasI = "false", hasB = "false";
@@ -683,7 +726,7 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
     if (S.n_aggs) {
       f += "    if (consumed) {\n";
-      for (auto& an : aggName[s]) f += "      " + an + "(ev, w, err);\n      if (err) { L.err = err; return; }\n";
+      for (auto& an : aggName[s]) f += "      " + an + "(ev, w, err, K);\n      if (err) { L.err = err; return; }\n";
       f += "    }\n";
     }
     f += "  }\n";
@@ -726,22 +769,28 @@ static std::string generate_jit(cep_query* q, Builder& b) {
     // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
     // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
     // One wave per key: the key's events are contiguous, so its loads coalesce.
+    // The begin predicate with null folds is true or throws at CSR position p, for any query
+    // of the launch (a group kernel: the union over its queries' constants; each lane still
+    // evaluates its own predicate there)
+    o += "__device__ __forceinline__ bool begin_hit_at(const NfaArgs& A, uint64_t p) {\n";
+    o += "  Ev e;\n  ld_bev(e, A, p);\n  const uint32_t nq = (NKC > 0 && A.n_q > 1) ? A.n_q : 1;\n";
+    o += "  for (uint32_t qi = 0; qi < nq; qi++) {\n    Kc K;\n    ld_kc(K, A, qi);\n    Fo f;\n";
+    o += "    f.nm = (1u << F) - 1;\n    int err = 0;\n";
+    o += "    if (" + predName[d.begin_stage][0] + "(e, f, err, K) || err) return true;\n  }\n  return false;\n}\n";
+    // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
+    // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
+    // One wave per key: the key's events are contiguous, so its loads coalesce.
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_est(NfaArgs A) {\n";
     o += "  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n  const uint32_t lane = threadIdx.x & 63;\n";
     o += "  if (k >= A.n_keys) return;\n";
     o += "  const uint64_t base = A.key_off[k];\n  const uint32_t n = (uint32_t)(A.key_off[k + 1] - base);\n";
-    o += "  uint64_t w = 0;\n  for (uint32_t j = lane; j < n; j += 64) {\n    Ev e;\n    ld_bev(e, A, base + j);\n";
-    o += "    Fo f;\n    f.nm = (1u << F) - 1;\n    int err = 0;\n";
-    o += "    const bool r = " + predName[d.begin_stage][0] + "(e, f, err);\n";
-    o += "    if (r || err) w += n - j;\n  }\n";
+    o += "  uint64_t w = 0;\n  for (uint32_t j = lane; j < n; j += 64)\n";
+    o += "    if (begin_hit_at(A, base + j)) w += n - j;\n";
     o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
     // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
     // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).
-    o += "__device__ __forceinline__ bool begin_hit_at(const NfaArgs& A, uint64_t p) {\n";
-    o += "  Ev e;\n  ld_bev(e, A, p);\n  Fo f;\n  f.nm = (1u << F) - 1;\n  int err = 0;\n";
-    o += "  return " + predName[d.begin_stage][0] + "(e, f, err) || err;\n}\n";
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_bits(NfaArgs A) {\n";
     o += "  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;\n";
     o += "  const uint64_t b = __ballot(p < A.n_events && begin_hit_at(A, p));\n";
@@ -777,7 +826,8 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   q->names.push_back("$final");
   uint16_t np = in.get<uint16_t>();
   if (np == 0) throw std::runtime_error("empty pattern");
-  std::vector<PatternIR> ps;
+  auto pq = std::make_shared<ParsedQuery>();  // kept for plan_groups
+  std::vector<PatternIR>& ps = pq->ps;
   for (int i = 0; i < np; i++) {
     PatternIR p;
     p.name = in.get<uint16_t>();
@@ -801,7 +851,8 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   q->info.n_fields = nf;
   q->info.n_states = ns;
 
-  Builder b{q, ps, {}, {}, {}};
+  pq->b.reset(new Builder{q, ps, {}, {}, {}});
+  Builder& b = *pq->b;
   // $final (StatesFactory.java:46-47)
   int successor = b.newStage((uint16_t)nn, ST_FINAL);
   const PatternIR* successorPattern = nullptr;
@@ -904,7 +955,51 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
     q->info.kind = CEP_KIND_NFA;
     q->info.arity = 0;
   }
-  q->jitSource = generate_jit(q, b);
+  LitCtx lits;
+  q->jitSource = generate_jit(q, b, lits);
+  q->parsed = pq;  // kept for kernel groups (plan_groups)
+}
+
+// Queries of a session that differ only in literal values share one kernel launch (a group):
+// lanes = (key, query), every wave one query of 64 keys, the literals that differ read from a
+// per-query table (NfaArgs.kc).  Groups keep first-appearance order; a query alone keeps its
+// own literal-inlined kernel.
+std::vector<GroupPlan> plan_groups(const std::vector<const cep_query*>& qs) {
+  const size_t n = qs.size();
+  std::vector<std::string> shape(n);
+  std::vector<std::vector<int64_t>> vals(n);
+  for (size_t i = 0; i < n; i++) {
+    LitCtx L;
+    L.param = true;
+    shape[i] = generate_jit(qs[i], *qs[i]->parsed->b, L);
+    vals[i] = L.values;
+  }
+  std::vector<GroupPlan> out;
+  std::vector<char> done(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    if (done[i]) continue;
+    GroupPlan g;
+    for (size_t j = i; j < n; j++)
+      if (!done[j] && shape[j] == shape[i]) {
+        g.members.push_back((int)j);
+        done[j] = 1;
+      }
+    if (g.members.size() == 1) {
+      g.source = qs[i]->jitSource;
+    } else {
+      std::vector<char> inl(vals[i].size(), 1);
+      for (int m : g.members)
+        for (size_t k = 0; k < inl.size(); k++) inl[k] = inl[k] && vals[m][k] == vals[i][k];
+      LitCtx L;
+      L.param = true;
+      L.inl = &inl;
+      g.source = generate_jit(qs[i], *qs[i]->parsed->b, L);
+      g.nkc = (uint32_t)L.values.size();
+      for (int m : g.members) g.table.insert(g.table.end(), vals[m].begin(), vals[m].end());
+    }
+    out.push_back(std::move(g));
+  }
+  return out;
 }
 
 }  // namespace cep

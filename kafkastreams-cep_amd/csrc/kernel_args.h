@@ -29,8 +29,14 @@ struct NfaArgs {
   void* walks;               // deferred-walk queues, wcap per slot (nfa_lane.h)
   uint32_t wcap;
   uint32_t defer;            // 1: queue buffer walks and drain them wave-wide; 0: walk in place
-  const uint32_t* key_list;  // retry pass: slot i runs key key_list[i]; null = all keys
-  uint32_t n_list;
+  // Jobs: a job is (query qi of the launch, key), id qi * n_keys + key.  Without a job list,
+  // wave W runs query W % n_q on the keys of ranks (W / n_q) * 64 + lane, rank -> key through
+  // `order` (lane order; null = identity).  A retry pass lists its jobs explicitly.
+  const uint32_t* jobs;      // retry pass: slot i runs job jobs[i]; null = the mapping above
+  uint32_t n_jobs;
+  const uint32_t* order;     // key of each rank (longest-first lane order), null = identity
+  uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
+  const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
   Node* nodes;
   Pred* preds;
   uint32_t* out;             // output chunks (kOutChunkWords words each)
@@ -41,7 +47,7 @@ struct NfaArgs {
   uint64_t* bhits;           // cep_nfa_bits: bit p = the begin predicate (null folds) is true or
                              // throws at CSR position p (quiet lanes jump to the next set bit)
   uint64_t n_events;         // CSR positions of the batch (bits kernel)
-  uint32_t* n_capacity_err;  // keys that hit CEP_KEY_CAPACITY
+  uint32_t* n_capacity_err;  // jobs to re-run (KE_RETRY / KE_CONFLICT)
 };
 
 }  // namespace cep

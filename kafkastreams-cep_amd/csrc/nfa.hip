@@ -51,6 +51,7 @@ struct InterpQ {
     return (sw & kRecEps) ? ((sw >> 8) & 0xFF) : q.st[sw & 0xFF].sk;
   }
   __device__ __forceinline__ uint16_t sk_name(uint32_t sk) const { return q.sk_name[sk]; }
+  __device__ __forceinline__ void set_query(uint32_t) {}  // one query per interpreter launch
 
   template <class LaneT>
   __device__ bool begin_pred(LaneT& lane) {
@@ -377,6 +378,17 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
   }
 }
 
+// jobs to re-run: KE_RETRY -> cap_list, KE_CONFLICT -> conf_list (any order: jobs are
+// independent); counts[0..1] their lengths
+__global__ void __launch_bounds__(256) collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list,
+                                                     uint32_t* conf_list, uint32_t* counts) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int e = ks[i].err;
+  if (e == KE_RETRY) cap_list[atomicAdd(counts, 1u)] = (uint32_t)i;
+  else if (e == KE_CONFLICT) conf_list[atomicAdd(counts + 1, 1u)] = (uint32_t)i;
+}
+
 // order-independent checksum of the flat match arrays (tests/gpu_helpers.py, bench.py and
 // multi-GPU all-gather): Σ_match mix(mix(C ^ key << 32 ^ emit) ^ (stage << 32 | seq) ...),
 // the same function as workloads.match_digest.  Fixed arity (m_emit == nullptr): match i's
@@ -453,6 +465,14 @@ hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* b
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_matches, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p, out,
                      m_key, m_emit, m_off, p_seq, p_stage, totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list, uint32_t* conf_list,
+                                uint32_t* counts, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(collect_retry, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, ks, n, cap_list, conf_list,
+                     counts);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 //   bool quiet                               the begin stage has a single BEGIN edge
 //   uint32_t begin_stage                     its stage index
 //   bool begin_pred(Lane&)                   its predicate on L.ev with all-null folds
+//   void set_query(uint32_t qi)              the lane's query within the launch (group kernels)
 //   uint32_t begin_scan(Lane&, j0, lim)      first position in [j0, lim) where begin_pred is
 //                                            true or throws (L.err set), else lim
 //   bool kBeginReg                           keep the begin run in registers (needs quiet)
@@ -65,6 +66,14 @@
 // walk's exception precedes anything the step did after queueing it.
 #pragma once
 #include "dewey.h"
+
+// Work counters for the CPU lane build (tests/lane_cpu, CEP_LANE_STATS); nothing on the GPU.
+#ifdef CEP_LANE_STATS
+extern uint64_t cep_lane_stats[8];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters
+#define CEP_STAT(i) (cep_lane_stats[i]++)
+#else
+#define CEP_STAT(i) ((void)0)
+#endif
 
 namespace cep {
 
@@ -266,7 +275,7 @@ struct Lane {
   // event's nodes exist: kPending, resolved at its next load.  Folds: set_folds.
   __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver) {
     if (ocount >= A.rcap) {
-      err = KE_CAPACITY;
+      err = KE_RETRY;
       return -1;
     }
     const uint32_t slot = ocount++;
@@ -305,6 +314,7 @@ struct Lane {
   // to loop forever on gfx950 (the loop-carried value never advanced); stores stay vectors.
   __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
     for (uint32_t i = first; i != CEP_NONE;) {
+      CEP_STAT(6);
       const Node& n = A.nodes[i];
       const uint32_t meta = n.meta, nx = n.same_next;
       if ((meta & 0xFF) == sk) return (meta & 0x100) ? i : CEP_NONE;
@@ -329,7 +339,7 @@ struct Lane {
     const uint32_t i = pool_take(A.node_pool, ncur, nend);
     const uint32_t p = i == CEP_NONE ? CEP_NONE : pool_take(A.pred_pool, pcur, pend);
     if (p == CEP_NONE) {
-      err = KE_CAPACITY;
+      err = KE_RETRY;
       return;
     }
     write_pred(p, prev, v);
@@ -342,7 +352,7 @@ struct Lane {
   __device__ __forceinline__ void append_pred(uint32_t node, uint32_t prev, const Dewey& v) {
     const uint32_t p = pool_take(A.pred_pool, pcur, pend);
     if (p == CEP_NONE) {
-      err = KE_CAPACITY;
+      err = KE_RETRY;
       return;
     }
     write_pred(p, prev, v);
@@ -362,7 +372,7 @@ struct Lane {
     }
     const uint32_t p = pool_take(A.pred_pool, pcur, pend);  // a new TimedKeyValue, one pointer
     if (p == CEP_NONE) {
-      err = KE_CAPACITY;
+      err = KE_RETRY;
       return;
     }
     write_pred(p, CEP_NONE, v);
@@ -400,6 +410,7 @@ struct Lane {
   // come back in prev / ver
   __device__ __forceinline__ uint32_t first_compat(uint32_t head, const Dewey& walker, uint32_t& prev, Dewey& ver) {
     for (uint32_t p = head; p != CEP_NONE;) {
+      CEP_STAT(4);
       const Pred& e0 = A.preds[p];
       const uint32_t fl = e0.flags, nxt = e0.next;
       if (!(fl & 1u)) {
@@ -433,7 +444,7 @@ struct Lane {
     if (ochunk == CEP_NONE || opos == kOutChunkWords - 1) {
       const uint32_t c = atomicAdd(A.out_pool.top, 1u);
       if (c >= A.out_pool.cap) {
-        err = KE_CAPACITY;
+        err = KE_RETRY;
         return 0;
       }
       if (ochunk == CEP_NONE) out_first = c;
@@ -450,12 +461,13 @@ struct Lane {
   // branch  KVSharedVersionedBuffer.java:99-110;  peek(remove=true)  :143-171 (emit: the
   // match construction's Sequence).  In place when !A.defer, else queued (see the header).
   __device__ __forceinline__ void walk(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v0) {
+    CEP_STAT(2);
     if (!A.defer) {
       walk_now(flags, sk, ev, first, v0, j);
       return;
     }
     if (wq_n >= A.wcap) {  // more walks in one event than the queue holds: re-run in place
-      err = KE_CAPACITY;
+      err = KE_RETRY;
       return;
     }
     const Dewey v = dw_pin(v0);
@@ -501,6 +513,7 @@ struct Lane {
       walk_fail(KE_NPE, t);
       return false;
     }
+    CEP_STAT(3);
     Node& n = A.nodes[s];
     const uint32_t ev_s = n.event, head = n.head, lk = n.lk;
     uint32_t meta = n.meta;
@@ -589,6 +602,7 @@ struct Lane {
   // Drains this lane's queue in order.  Called by every lane of the wave at once: the loop
   // gives each lane one node per iteration, starting its next walk as soon as one ends.
   __device__ __forceinline__ void flush() {
+    CEP_STAT(5);
     const uint32_t id0 = opc - wq_n;
     uint32_t i = 0, s = CEP_NONE, t = 0, flags = 0, np = 0;
     uint64_t npa = 0;
@@ -619,6 +633,7 @@ struct Lane {
         if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
         active = true;
       }
+      CEP_STAT(7);
       if (!walk_node(flags, s, w, t, id0 + i - 1, np)) {
         if (err) break;
         walk_end(flags, npa, np);
@@ -630,6 +645,7 @@ struct Lane {
 
   // ---------------------------------------------------------------- one event
   __device__ __forceinline__ void event(bool begin_hit) {
+    CEP_STAT(0);
     const uint32_t pf = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
     n_final = 0;
@@ -641,6 +657,7 @@ struct Lane {
     const uint32_t n = count;
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
+      CEP_STAT(1);
       load(half, i, c, pf);
       const int produced = q.step(*this, c);
       if (err) return;
@@ -779,9 +796,20 @@ struct Lane {
 template <int F, class Q>
 __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullptr) {
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nslots = A.key_list ? A.n_list : A.n_keys;
-  if (slot >= nslots) return;
-  const uint32_t key = A.key_list ? A.key_list[slot] : (uint32_t)slot;
+  uint64_t job;
+  if (A.jobs) {
+    if (slot >= A.n_jobs) return;
+    job = A.jobs[slot];
+  } else {
+    const uint32_t nq = A.n_q ? A.n_q : 1;
+    const uint64_t w = slot / 64;
+    const uint64_t rank = (w / nq) * 64 + slot % 64;
+    if (rank >= A.n_keys) return;
+    job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
+  }
+  const uint32_t qi = (uint32_t)(job / A.n_keys);
+  const uint32_t key = (uint32_t)(job % A.n_keys);
+  q.set_query(qi);
   Lane<F, Q> L(A, q);
   L.key = key;
   L.n_ev = (uint32_t)(A.key_off[key + 1] - A.key_off[key]);
@@ -790,8 +818,8 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);
-  KeyState& ks = A.ks[key];
-  KeyCarry* kc = A.carry ? A.carry + key : nullptr;
+  KeyState& ks = A.ks[job];
+  KeyCarry* kc = A.carry ? A.carry + job : nullptr;
   if (kc && kc->live) {  // the key's NFA as the previous batch left it
     if (kc->err) {        // stopped by an exception: stays stopped
       ks.n_matches = ks.n_pairs = 0;
@@ -833,7 +861,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   ks.out_first = L.out_first;
   ks.err = L.err;
   ks.err_seq = L.err_seq;
-  if (L.err == KE_CAPACITY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
+  if (L.err == KE_RETRY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
   if (kc) {
     if (!L.err) L.lds_spill(true);  // LDS ends with the launch: the queue continues from HBM
     kc->live = 1;

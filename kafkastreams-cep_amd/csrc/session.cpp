@@ -91,21 +91,12 @@ struct QueryRt {
   const cep_query* q;
   int F = 2;
   DBuf d_q, d_code;
-  hipModule_t mod = nullptr;  // JIT tier: the query's own nfa kernel (cep_nfa_jit)
-  hipFunction_t fn = nullptr;
-  hipFunction_t fn_est = nullptr;  // cep_nfa_est (queries whose begin stage has one BEGIN edge)
-  hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
-  double jit_compile_s = 0;
-  DBuf est, order, order_tmp, est_sorted;
-  void* sort_tmp = nullptr;  // hipCUB scratch of the lane-order sort
-  size_t sort_tmp_bytes = 0;
-  ~QueryRt() {
-    if (mod) (void)hipModuleUnload(mod);
-    if (sort_tmp) (void)hipFree(sort_tmp);
-  }
+  int group = -1;   // kernel group (NFA path), -1: stencil
+  uint32_t qi = 0;  // index within the group
   // results of the last batch (device)
   DBuf m_key, m_emit, m_off, p_seq, p_stage;
-  DBuf ks;
+  DBuf ks;                      // stencil path: per-key state (all zero)
+  const KeyState* ks_dev = nullptr;  // this query's KeyState[n_keys] (the group's slice or ks)
   uint64_t n_matches = 0, n_pairs = 0;
   unsigned long long digest = 0;
   bool digest_valid = false;  // computed on demand (cep_match_digest)
@@ -116,10 +107,35 @@ struct QueryRt {
   std::vector<uint64_t> h_off;
   std::vector<uint16_t> h_stage;
   bool host_valid = false;
-  float kernel_ms = 0;  // the matching kernel (nfa_kernel / stencil_kernel) launches
+  float kernel_ms = 0;  // the matching kernel launches (a group's launches, shared by its queries)
   float aux_ms = 0;     // setup and compaction kernels of the same batch
   uint32_t launches = 0;
   StreamState st;
+};
+
+// Queries whose NFA kernels run as one launch (compile.cpp plan_groups): lanes are (query,
+// key) jobs, wave W runs query W % Q on 64 keys, so the Q waves of a key group read its
+// event columns together (one HBM read, L2 hits for the rest).
+struct GroupRt {
+  std::vector<int> members;
+  int F = 2;
+  hipModule_t mod = nullptr;  // JIT tier: the group's kernel (cep_nfa_jit)
+  hipFunction_t fn = nullptr;
+  hipFunction_t fn_est = nullptr;   // cep_nfa_est (begin stage = one BEGIN edge)
+  hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
+  double jit_compile_s = 0;
+  DBuf kc;  // literal table, Q x nkc
+  DBuf ks;  // KeyState[Q x n_keys]
+  DBuf est, order, order_tmp, est_sorted;
+  void* sort_tmp = nullptr;  // lane-order sort scratch
+  size_t sort_tmp_bytes = 0;
+  // pool use of the last batch (the next batch's pools are sized from it)
+  uint64_t last_nodes = 0, last_preds = 0, last_out = 0;
+  cep_batch_stats stats{};  // the last batch
+  ~GroupRt() {
+    if (mod) (void)hipModuleUnload(mod);
+    if (sort_tmp) (void)hipFree(sort_tmp);
+  }
 };
 
 }  // namespace
@@ -130,6 +146,7 @@ struct cep_session {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   std::vector<std::unique_ptr<QueryRt>> qs;
+  std::vector<std::unique_ptr<GroupRt>> groups;
   // batch (device copies when the batch is host-resident)
   DBuf b_off, b_ts;
   DBuf b_cols[kMaxFields];
@@ -147,7 +164,7 @@ struct cep_session {
   std::vector<uint32_t> h_perm;
   bool layout_host_valid = false;
   // scratch
-  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask, bhits;
+  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
 };
 
 namespace {
@@ -163,7 +180,7 @@ struct DeviceGuard {
 
 struct Scratch {  // small counters, one allocation
   uint32_t node_top, pred_top, out_top, n_cap_err;
-  uint32_t tile_counter, overflow, pad0, pad1;
+  uint32_t tile_counter, overflow, n_retry_cap, n_retry_conflict;
   uint64_t totals[2];
   uint64_t total;
   unsigned long long digest;
@@ -243,47 +260,67 @@ void run_stencil(cep_session* s, QueryRt& r) {
   // no per-key errors on this path: the predicates and folds are total
   r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
   HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * nk, s->stream));
+  r.ks_dev = r.ks.as<KeyState>();
   HIPCHECK(hipStreamSynchronize(s->stream));
 }
 
-hipError_t launch_nfa_tier(QueryRt& r, NfaArgs& a, uint64_t nslots, hipStream_t st) {
-  if (!r.fn) return launch_nfa(r.F, a, nslots, r.q->dev.code_len, st);
+hipError_t launch_nfa_tier(GroupRt& g, const cep_query* q0, NfaArgs& a, uint64_t nslots, hipStream_t st) {
+  if (!g.fn) return launch_nfa(g.F, a, nslots, q0->dev.code_len, st);
   if (nslots == 0) return hipSuccess;
   size_t size = sizeof(NfaArgs);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-  return hipModuleLaunchKernel(r.fn, (uint32_t)((nslots + 255) / 256), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return hipModuleLaunchKernel(g.fn, (uint32_t)((nslots + 255) / 256), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
-void run_nfa(cep_session* s, QueryRt& r) {
+hipError_t launch_fn(hipFunction_t fn, NfaArgs& a, uint64_t blocks, hipStream_t st) {
+  size_t size = sizeof(NfaArgs);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  return hipModuleLaunchKernel(fn, (uint32_t)blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
+constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;  // pool indices are u32
+
+// Runs a kernel group over the batch: the begin-hit bitmap and lane order, the matching
+// launch, re-runs of the jobs that hit a capacity limit or a deferred-walk conflict, and the
+// per-query compaction of the output chains into flat arrays.
+void run_nfa(cep_session* s, GroupRt& g) {
   const uint64_t nk = s->n_keys;
+  const uint64_t Q = g.members.size();
+  const uint64_t jobs = Q * nk;
+  QueryRt& r0 = *s->qs[g.members[0]];
   uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
-  const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.25;
-  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
+  const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.0625;
+  const uint64_t slots = ((nk + 63) / 64) * 64 * Q;  // Q waves per 64-key group
+  g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
 
-  // pools: nodes / preds ~ pool_factor per event (+ chunk slack per key); output chunks
+  // Pools: nodes / preds / output chunks, shared by the group's jobs.  Sized from the last
+  // batch's use when there is one (x1.5), else from pool_factor per event and query; a job
+  // that runs out is re-run below with grown pools.
   const uint32_t nchunk = 16, pchunk = 16;
-  uint64_t node_cap = (uint64_t)(pf * (double)s->n_events) + nk * nchunk + 4096;
-  uint64_t pred_cap = (uint64_t)(pf * (double)s->n_events) + nk * pchunk + 4096;
-  uint64_t out_cap = (uint64_t)(pf * (double)s->n_events * 2 / kOutChunkWords) + nk / 4 + 1024;
-  node_cap = std::min<uint64_t>(node_cap, 0xFFFFFFF0ull);
-  pred_cap = std::min<uint64_t>(pred_cap, 0xFFFFFFF0ull);
-  out_cap = std::min<uint64_t>(out_cap, 0xFFFFFFF0ull / kOutChunkWords);
+  const uint64_t ev_q = (uint64_t)((double)s->n_events * (double)Q);
+  uint64_t node_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_nodes * 3 / 2 + 4096);
+  uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_preds * 3 / 2 + 4096);
+  uint64_t out_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q * 2 / kOutChunkWords) + jobs / 64 + 1024,
+                                        g.last_out * 3 / 2 + 1024);
+  node_cap = std::min<uint64_t>(node_cap, kPoolMax);
+  pred_cap = std::min<uint64_t>(pred_cap, kPoolMax);
+  out_cap = std::min<uint64_t>(out_cap, kPoolMax);  // chunk ids are u32, word addresses u64
   s->nodes.ensure(sizeof(Node) * node_cap);
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
-  s->rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
+  s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
   // deferred walks a key can queue (nfa_lane.h drains at CEP_WALK_FLUSH; $CEP_WALK_CAP: tuning)
   uint32_t wcap = 64;
   if (const char* e = std::getenv("CEP_WALK_CAP"))
     if (std::atoi(e) > 0) wcap = (uint32_t)std::atoi(e);
-  s->walks.ensure(walkq_size(std::max<uint64_t>(nk, 1), wcap));
+  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
-  const bool streaming = s->opts.streaming != 0;
-  StreamState& S = r.st;
+  const bool streaming = s->opts.streaming != 0;  // (a streaming group holds one query)
+  StreamState& S = r0.st;
   if (streaming) {
     if (!S.init) {
       S.n_keys = nk;
@@ -291,9 +328,9 @@ void run_nfa(cep_session* s, QueryRt& r) {
       HIPCHECK(hipMemsetAsync(S.carry.p, 0, sizeof(KeyCarry) * std::max<uint64_t>(nk, 1), s->stream));
       S.tops.ensure(2 * sizeof(uint32_t));
       HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
-      S.rings.ensure(ring_size(r.F, std::max<uint64_t>(nk, 1), rcap));
+      S.rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
       S.rcap = rcap;
-      S.ring_bytes = ring_size(r.F, std::max<uint64_t>(nk, 1), rcap);
+      S.ring_bytes = ring_size(g.F, std::max<uint64_t>(slots, 1), rcap);
       S.init = true;
     } else if (nk != S.n_keys) {
       throw std::invalid_argument("the batches of a streaming session share one key space (n_keys)");
@@ -301,23 +338,23 @@ void run_nfa(cep_session* s, QueryRt& r) {
     // a stream cannot re-run a key (its state moved on): size the pools for this batch on top
     // of what the stream already holds, generously (capacity errors would be final)
     const uint64_t add = s->n_events + nk * 2 * nchunk + 4096;
-    const uint64_t nn = std::min<uint64_t>(S.node_used + add, 0xFFFFFFF0ull);
-    const uint64_t pn = std::min<uint64_t>(S.pred_used + add, 0xFFFFFFF0ull);
+    const uint64_t nn = std::min<uint64_t>(S.node_used + add, kPoolMax);
+    const uint64_t pn = std::min<uint64_t>(S.pred_used + add, kPoolMax);
     if (nn > S.node_cap) {
-      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), 0xFFFFFFF0ull);
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), kPoolMax);
       S.nodes.grow_keep(sizeof(Node) * c, sizeof(Node) * S.node_used, s->stream);
       S.node_cap = c;
     }
     if (pn > S.pred_cap) {
-      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(pn, S.pred_cap * 3 / 2), 0xFFFFFFF0ull);
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(pn, S.pred_cap * 3 / 2), kPoolMax);
       S.preds.grow_keep(sizeof(Pred) * c, sizeof(Pred) * S.pred_used, s->stream);
       S.pred_cap = c;
     }
-    out_cap = std::max<uint64_t>(out_cap, std::min<uint64_t>(nk + s->n_events / 64 + 1024, 0xFFFFFFF0ull / kOutChunkWords));
+    out_cap = std::max<uint64_t>(out_cap, std::min<uint64_t>(nk + s->n_events / 64 + 1024, kPoolMax));
     s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   }
-  a.q = r.d_q.as<DevQuery>();
-  a.code = r.d_code.as<uint32_t>();
+  a.q = r0.d_q.as<DevQuery>();
+  a.code = r0.d_code.as<uint32_t>();
   a.n_keys = nk;
   a.key_off = s->key_off;
   a.cols = s->cols;
@@ -327,16 +364,17 @@ void run_nfa(cep_session* s, QueryRt& r) {
   a.walks = s->walks.p;
   a.wcap = wcap;
   a.defer = 1;
-  a.key_list = nullptr;
-  a.n_list = 0;
+  a.n_q = (uint32_t)Q;
+  a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
   a.preds = s->preds.as<Pred>();
   a.out = s->out.as<uint32_t>();
   a.node_pool = Pool{&sc->node_top, (uint32_t)node_cap, nchunk};
   a.pred_pool = Pool{&sc->pred_top, (uint32_t)pred_cap, pchunk};
   a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, 1};
-  a.ks = r.ks.as<KeyState>();
+  a.ks = g.ks.as<KeyState>();
   a.n_capacity_err = &sc->n_cap_err;
+  a.n_events = s->n_events;
   if (streaming) {  // walks in place: a conflict could not be re-run (nfa_lane.h)
     a.defer = 0;
     a.rings = S.rings.p;
@@ -348,38 +386,31 @@ void run_nfa(cep_session* s, QueryRt& r) {
   }
 
   float total_ms = 0;
-  r.launches = 0;
+  uint32_t launches = 0;
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
   // Lane order: keys sorted by estimated work, longest first (cep_nfa_est), so a wave's 64
   // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
   // start first.  Streams keep the identity order (their run queues live at the key's slot).
-  if (r.fn_est && !streaming && nk > 64) {
-    r.est.ensure(4 * nk);
-    r.est_sorted.ensure(4 * nk);
-    r.order.ensure(4 * nk);
-    r.order_tmp.ensure(4 * nk);
-    a.est = r.est.as<uint32_t>();
-    size_t size = sizeof(NfaArgs);
-    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    HIPCHECK(hipModuleLaunchKernel(r.fn_est, (uint32_t)((nk + 3) / 4), 1, 1, 256, 1, 1, 0, s->stream, nullptr,
-                                   cfg));  // a wave per key
-    HIPCHECK(sort_keys_by_work(r.est.as<uint32_t>(), r.est_sorted.as<uint32_t>(), r.order_tmp.as<uint32_t>(),
-                               r.order.as<uint32_t>(), nk, r.sort_tmp, r.sort_tmp_bytes, s->stream));
-    a.key_list = r.order.as<uint32_t>();
-    a.n_list = (uint32_t)nk;
+  if (g.fn_est && !streaming && nk > 64) {
+    g.est.ensure(4 * nk);
+    g.est_sorted.ensure(4 * nk);
+    g.order.ensure(4 * nk);
+    g.order_tmp.ensure(4 * nk);
+    a.est = g.est.as<uint32_t>();
+    HIPCHECK(launch_fn(g.fn_est, a, (nk + 3) / 4, s->stream));  // a wave per key
+    HIPCHECK(sort_keys_by_work(g.est.as<uint32_t>(), g.est_sorted.as<uint32_t>(), g.order_tmp.as<uint32_t>(),
+                               g.order.as<uint32_t>(), nk, g.sort_tmp, g.sort_tmp_bytes, s->stream));
+    a.order = g.order.as<uint32_t>();
   }
-  a.n_events = s->n_events;
-  if (r.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
+  if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
     s->bhits.ensure(8 * ((s->n_events + 63) / 64));
     a.bhits = s->bhits.as<uint64_t>();
-    size_t size = sizeof(NfaArgs);
-    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    HIPCHECK(hipModuleLaunchKernel(r.fn_bits, (uint32_t)((s->n_events + 255) / 256), 1, 1, 256, 1, 1, 0, s->stream,
-                                   nullptr, cfg));
+    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 255) / 256, s->stream));
   }
-  HIPCHECK(launch_nfa_tier(r, a, nk, s->stream));
+  HIPCHECK(hipEventRecord(s->ev2, s->stream));
+  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
-  r.launches++;
+  launches++;
   Scratch h{};
   HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
@@ -393,93 +424,119 @@ void run_nfa(cep_session* s, QueryRt& r) {
     S.pred_used = (uint32_t)std::min<uint64_t>(tops[1], S.pred_cap);
     h.n_cap_err = 0;
   }
+  g.last_nodes = h.node_top;
+  g.last_preds = h.pred_top;
+  g.last_out = h.out_top;
 
-  // retry keys that hit a capacity limit with 8x the live-run ring and grown pools, and
-  // keys whose deferred walks conflicted (KE_CONFLICT), with walks in place
-  for (int round = 0; h.n_cap_err > 0 && round < 3; round++) {
-    std::vector<KeyState> hks(nk);
-    HIPCHECK(hipMemcpyAsync(hks.data(), r.ks.p, sizeof(KeyState) * nk, hipMemcpyDeviceToHost, s->stream));
-    HIPCHECK(hipStreamSynchronize(s->stream));
-    std::vector<uint32_t> list;
-    for (uint64_t k = 0; k < nk; k++)
-      if (hks[k].err == KE_CAPACITY || hks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
-    if (list.empty()) break;
-    rcap *= 8;
-    s->keylist.ensure(sizeof(uint32_t) * list.size());
-    HIPCHECK(hipMemcpyAsync(s->keylist.p, list.data(), sizeof(uint32_t) * list.size(), hipMemcpyHostToDevice,
-                            s->stream));
-    // grow pools (indices stay valid: copy the used prefix)
-    const uint64_t extra_events = 0;
-    (void)extra_events;
-    uint64_t nn = std::min<uint64_t>(node_cap * 2 + (uint64_t)list.size() * 4096, 0xFFFFFFF0ull);
-    uint64_t pn = std::min<uint64_t>(pred_cap * 2 + (uint64_t)list.size() * 4096, 0xFFFFFFF0ull);
-    uint64_t on = std::min<uint64_t>(out_cap * 2 + (uint64_t)list.size() * 64, 0xFFFFFFF0ull / kOutChunkWords);
+  // Re-run the jobs that hit a capacity limit (with 8x the run queue and 4x every exhausted
+  // pool; walks still deferred) and those whose deferred walks conflicted (walks in place).
+  // The job lists are collected on the device; only their lengths come back.
+  g.stats = cep_batch_stats{};
+  g.stats.group_queries = (uint32_t)Q;
+  float main_ms = 0;
+  HIPCHECK(hipEventElapsedTime(&main_ms, s->ev2, s->ev1));
+  g.stats.main_ms = main_ms;
+  for (int round = 0; h.n_cap_err > 0 && round < 8; round++) {
+    const uint64_t nlist = h.n_cap_err;
+    s->keylist.ensure(sizeof(uint32_t) * 2 * nlist);
+    uint32_t* cap_list = s->keylist.as<uint32_t>();
+    uint32_t* conf_list = cap_list + nlist;
+    HIPCHECK(launch_collect_retry(g.ks.as<KeyState>(), jobs, cap_list, conf_list, &sc->n_retry_cap, s->stream));
+    // grow every pool a job ran out of (indices of the used prefix stay valid)
+    const bool node_full = h.node_top >= node_cap - nchunk, pred_full = h.pred_top >= pred_cap - pchunk;
+    const bool out_full = h.out_top >= out_cap;
+    const uint64_t nn = node_full ? std::min<uint64_t>(node_cap * 4 + nlist * 64, kPoolMax) : node_cap;
+    const uint64_t pn = pred_full ? std::min<uint64_t>(pred_cap * 4 + nlist * 64, kPoolMax) : pred_cap;
+    const uint64_t on = out_full ? std::min<uint64_t>(out_cap * 4 + nlist, kPoolMax) : out_cap;
     s->nodes.grow_keep(sizeof(Node) * nn, sizeof(Node) * std::min<uint64_t>(h.node_top, node_cap), s->stream);
     s->preds.grow_keep(sizeof(Pred) * pn, sizeof(Pred) * std::min<uint64_t>(h.pred_top, pred_cap), s->stream);
     s->out.grow_keep(sizeof(uint32_t) * kOutChunkWords * on,
                      sizeof(uint32_t) * kOutChunkWords * std::min<uint64_t>(h.out_top, out_cap), s->stream);
-    Scratch fix = h;  // pool tops may have run past the caps; restart them at the old caps
+    Scratch fix{};  // pool tops may have run past the caps; restart them at the old caps
     fix.node_top = (uint32_t)std::min<uint64_t>(h.node_top, node_cap);
     fix.pred_top = (uint32_t)std::min<uint64_t>(h.pred_top, pred_cap);
     fix.out_top = (uint32_t)std::min<uint64_t>(h.out_top, out_cap);
-    fix.n_cap_err = 0;
+    uint32_t lens[2];
+    HIPCHECK(hipMemcpyAsync(lens, &sc->n_retry_cap, sizeof lens, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    HIPCHECK(hipMemcpyAsync(sc, &fix, sizeof fix, hipMemcpyHostToDevice, s->stream));
     node_cap = nn;
     pred_cap = pn;
     out_cap = on;
-    DBuf retry_rings;
-    retry_rings.ensure(ring_size(r.F, list.size(), rcap));
-    HIPCHECK(hipMemcpyAsync(sc, &fix, sizeof fix, hipMemcpyHostToDevice, s->stream));
     a.nodes = s->nodes.as<Node>();
     a.preds = s->preds.as<Pred>();
     a.out = s->out.as<uint32_t>();
     a.node_pool.cap = (uint32_t)node_cap;
     a.pred_pool.cap = (uint32_t)pred_cap;
     a.out_pool.cap = (uint32_t)out_cap;
-    a.rings = retry_rings.p;
+    // a bigger run queue per retried job, its ring kept within 16 GiB
+    rcap *= 8;
+    const uint64_t most = std::max<uint64_t>(lens[0], lens[1]);
+    while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
     a.rcap = rcap;
-    a.defer = 0;
-    a.key_list = s->keylist.as<uint32_t>();
-    a.n_list = (uint32_t)list.size();
+    s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
+    a.rings = s->retry_rings.p;
+    a.order = nullptr;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
-    HIPCHECK(launch_nfa_tier(r, a, list.size(), s->stream));
+    for (int k = 0; k < 2; k++) {  // capacity re-runs keep deferred walks, conflicts walk in place
+      if (!lens[k]) continue;
+      a.defer = k == 0 ? 1 : 0;
+      a.jobs = k == 0 ? cap_list : conf_list;
+      a.n_jobs = lens[k];
+      HIPCHECK(launch_nfa_tier(g, r0.q, a, lens[k], s->stream));
+      launches++;
+      g.stats.retried_jobs += lens[k];
+    }
     HIPCHECK(hipEventRecord(s->ev1, s->stream));
-    r.launches++;
     HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
     HIPCHECK(hipStreamSynchronize(s->stream));
     HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     total_ms += ms;
+    g.stats.retry_ms += ms;
+    g.last_nodes = h.node_top;
+    g.last_preds = h.pred_top;
+    g.last_out = h.out_top;
   }
 
-  // compaction: scans of per-key counts, then the scatter into flat arrays
+  g.stats.kernel_ms = total_ms;
+  g.stats.launches = launches;
+  g.stats.nodes_used = std::min<uint64_t>(h.node_top, node_cap);
+  g.stats.preds_used = std::min<uint64_t>(h.pred_top, pred_cap);
+  g.stats.out_chunks_used = std::min<uint64_t>(h.out_top, out_cap);
+  // compaction per query: scans of per-key counts, then the scatter into flat arrays
   const uint64_t nb = (nk + 255) / 256;
-  DBuf bsum;
-  bsum.ensure(sizeof(uint64_t) * 2 * (nb + 1));
-  uint64_t* bm = bsum.as<uint64_t>();
+  s->bsum.ensure(sizeof(uint64_t) * 2 * (nb + 1));
+  uint64_t* bm = s->bsum.as<uint64_t>();
   uint64_t* bp = bm + nb + 1;
-  HIPCHECK(hipEventRecord(s->ev0, s->stream));
-  HIPCHECK(launch_compact(r.ks.as<KeyState>(), nk, bm, bp, sc->totals, s->stream));
-  uint64_t tot[2] = {0, 0};
-  HIPCHECK(hipMemcpyAsync(tot, sc->totals, sizeof tot, hipMemcpyDeviceToHost, s->stream));
-  HIPCHECK(hipStreamSynchronize(s->stream));
-  r.n_matches = tot[0];
-  r.n_pairs = tot[1];
-  r.m_key.ensure(sizeof(uint32_t) * (tot[0] + 1));
-  r.m_emit.ensure(sizeof(uint32_t) * (tot[0] + 1));
-  r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));
-  r.p_seq.ensure(sizeof(uint32_t) * (tot[1] + 1));
-  r.p_stage.ensure(sizeof(uint16_t) * (tot[1] + 1));
-  HIPCHECK(launch_scatter(r.ks.as<KeyState>(), nk, bm, bp, s->out.as<uint32_t>(), r.m_key.as<uint32_t>(),
-                          r.m_emit.as<uint32_t>(), r.m_off.as<uint64_t>(), r.p_seq.as<uint32_t>(),
-                          r.p_stage.as<uint16_t>(), sc->totals, s->stream));
-  if (nk == 0) HIPCHECK(hipMemsetAsync(r.m_off.p, 0, sizeof(uint64_t), s->stream));
-  HIPCHECK(hipEventRecord(s->ev1, s->stream));
-  HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
-  HIPCHECK(hipStreamSynchronize(s->stream));
-  HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
-  r.aux_ms = ms;  // compaction (count/scan/scatter)
-  r.digest_valid = false;
-  r.arity = 0;
-  r.kernel_ms = total_ms;  // matching kernel launches only
+  for (uint64_t qi = 0; qi < Q; qi++) {
+    QueryRt& r = *s->qs[g.members[qi]];
+    const KeyState* ks = g.ks.as<KeyState>() + qi * nk;
+    r.ks_dev = ks;
+    HIPCHECK(hipEventRecord(s->ev0, s->stream));
+    HIPCHECK(launch_compact(ks, nk, bm, bp, sc->totals, s->stream));
+    uint64_t tot[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(tot, sc->totals, sizeof tot, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    r.n_matches = tot[0];
+    r.n_pairs = tot[1];
+    r.m_key.ensure(sizeof(uint32_t) * (tot[0] + 1));
+    r.m_emit.ensure(sizeof(uint32_t) * (tot[0] + 1));
+    r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));
+    r.p_seq.ensure(sizeof(uint32_t) * (tot[1] + 1));
+    r.p_stage.ensure(sizeof(uint16_t) * (tot[1] + 1));
+    HIPCHECK(launch_scatter(ks, nk, bm, bp, s->out.as<uint32_t>(), r.m_key.as<uint32_t>(), r.m_emit.as<uint32_t>(),
+                            r.m_off.as<uint64_t>(), r.p_seq.as<uint32_t>(), r.p_stage.as<uint16_t>(), sc->totals,
+                            s->stream));
+    if (nk == 0) HIPCHECK(hipMemsetAsync(r.m_off.p, 0, sizeof(uint64_t), s->stream));
+    HIPCHECK(hipEventRecord(s->ev1, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    r.aux_ms = ms;  // compaction (count/scan/scatter)
+    r.digest_valid = false;
+    r.arity = 0;
+    r.kernel_ms = total_ms;  // the group's matching launches
+    r.launches = launches;
+  }
 }
 
 int guarded(const std::function<void()>& f) {
@@ -538,6 +595,58 @@ int cep_jit_precompile(const cep_query* q, double* compile_s) {
   return CEP_OK;
 }
 
+int cep_jit_precompile_group(const cep_query* const* queries, int n_queries, double* compile_s) {
+  if (!queries || n_queries <= 0) return fail(CEP_E_INVALID, "need at least one query");
+  std::vector<const cep_query*> qv;
+  for (int i = 0; i < n_queries; i++) {
+    if (!queries[i]) return fail(CEP_E_INVALID, "null query");
+    if (!queries[i]->info.compile_error) qv.push_back(queries[i]);
+  }
+  if (compile_s) *compile_s = 0;
+  try {
+    for (auto& pl : plan_groups(qv)) {
+      double t = 0;
+      jit_code_object(pl.source, &t);
+      if (compile_s) *compile_s += t;
+    }
+  } catch (std::exception& e) {
+    return fail(CEP_E_COMPILE, e.what());
+  }
+  return CEP_OK;
+}
+
+int cep_query_group_plan(const cep_query* const* queries, int n_queries, int group, const char** source,
+                         uint32_t* n_members, const int32_t** members, uint32_t* n_literals,
+                         const int64_t** literals) {
+  thread_local GroupPlan plan;
+  thread_local std::vector<int32_t> mem;
+  if (!queries || n_queries <= 0 || group < 0) return fail(CEP_E_INVALID, "bad argument");
+  std::vector<const cep_query*> qv;
+  std::vector<int> idx;
+  for (int i = 0; i < n_queries; i++) {
+    if (!queries[i]) return fail(CEP_E_INVALID, "null query");
+    if (!queries[i]->info.compile_error) {
+      qv.push_back(queries[i]);
+      idx.push_back(i);
+    }
+  }
+  try {
+    auto plans = plan_groups(qv);
+    if (group >= (int)plans.size()) return fail(CEP_E_INVALID, "no such group");
+    plan = std::move(plans[group]);
+  } catch (std::exception& e) {
+    return fail(CEP_E_COMPILE, e.what());
+  }
+  mem.clear();
+  for (int m : plan.members) mem.push_back(idx[m]);
+  if (source) *source = plan.source.c_str();
+  if (n_members) *n_members = (uint32_t)mem.size();
+  if (members) *members = mem.data();
+  if (n_literals) *n_literals = plan.nkc;
+  if (literals) *literals = plan.table.data();
+  return CEP_OK;
+}
+
 int cep_session_create(const cep_query* const* queries, int n_queries, const cep_opts* opts, cep_session** out) {
   if (!queries || n_queries <= 0 || !out) return fail(CEP_E_INVALID, "need at least one query");
   for (int i = 0; i < n_queries; i++) {
@@ -567,17 +676,50 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
       r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());
       HIPCHECK(hipMemcpy(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
                          hipMemcpyHostToDevice));
-      const bool nfa = queries[i]->info.kind == CEP_KIND_NFA || s->opts.force_nfa || s->opts.streaming;
-      if (nfa && s->opts.tier == CEP_TIER_JIT) {  // the query's own kernel, compiled by hipRTC
-        std::vector<char> co = jit_code_object(queries[i]->jitSource, &r->jit_compile_s);
-        HIPCHECK(hipModuleLoadData(&r->mod, co.data()));
-        HIPCHECK(hipModuleGetFunction(&r->fn, r->mod, "cep_nfa_jit"));
-        if (queries[i]->jitSource.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
-          HIPCHECK(hipModuleGetFunction(&r->fn_est, r->mod, "cep_nfa_est"));
-          HIPCHECK(hipModuleGetFunction(&r->fn_bits, r->mod, "cep_nfa_bits"));
+      s->qs.push_back(std::move(r));
+    }
+    // kernel groups: the JIT tier of a per-batch session runs queries that differ only in
+    // literals as one launch (plan_groups); streams and the interpreter run one query each
+    std::vector<int> nfa;
+    for (int i = 0; i < n_queries; i++)
+      if (queries[i]->info.kind == CEP_KIND_NFA || s->opts.force_nfa || s->opts.streaming) nfa.push_back(i);
+    std::vector<GroupPlan> plans;
+    if (s->opts.tier == CEP_TIER_JIT && !s->opts.streaming && !s->opts.no_groups) {
+      std::vector<const cep_query*> qv;
+      for (int i : nfa) qv.push_back(queries[i]);
+      plans = plan_groups(qv);
+      for (auto& pl : plans)
+        for (int& m : pl.members) m = nfa[m];
+    } else {
+      for (int i : nfa) {
+        GroupPlan pl;
+        pl.members.push_back(i);
+        pl.source = queries[i]->jitSource;
+        plans.push_back(std::move(pl));
+      }
+    }
+    for (auto& pl : plans) {
+      auto g = std::make_unique<GroupRt>();
+      g->members = pl.members;
+      g->F = s->qs[pl.members[0]]->F;
+      for (size_t k = 0; k < pl.members.size(); k++) {
+        s->qs[pl.members[k]]->group = (int)s->groups.size();
+        s->qs[pl.members[k]]->qi = (uint32_t)k;
+      }
+      if (s->opts.tier == CEP_TIER_JIT) {  // the group's own kernel, compiled by hipRTC
+        std::vector<char> co = jit_code_object(pl.source, &g->jit_compile_s);
+        HIPCHECK(hipModuleLoadData(&g->mod, co.data()));
+        HIPCHECK(hipModuleGetFunction(&g->fn, g->mod, "cep_nfa_jit"));
+        if (pl.source.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
+          HIPCHECK(hipModuleGetFunction(&g->fn_est, g->mod, "cep_nfa_est"));
+          HIPCHECK(hipModuleGetFunction(&g->fn_bits, g->mod, "cep_nfa_bits"));
         }
       }
-      s->qs.push_back(std::move(r));
+      if (pl.nkc) {
+        g->kc.ensure(sizeof(int64_t) * pl.table.size());
+        HIPCHECK(hipMemcpy(g->kc.p, pl.table.data(), sizeof(int64_t) * pl.table.size(), hipMemcpyHostToDevice));
+      }
+      s->groups.push_back(std::move(g));
     }
   });
   if (rc) return rc;
@@ -590,6 +732,7 @@ void cep_session_destroy(cep_session* s) {
   {
     DeviceGuard g(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    s->groups.clear();
     s->qs.clear();
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -716,12 +859,12 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       HIPCHECK(hipStreamSynchronize(s->stream));
       s->watermark = (int64_t)(w ^ 0x8000000000000000ull);
     }
-    for (auto& r : s->qs) {
-      // a stream carries NFA state between batches: stencil queries run on the NFA there
-      if (r->q->info.kind == CEP_KIND_STENCIL && !s->opts.force_nfa && !s->opts.streaming) run_stencil(s, *r);
-      else run_nfa(s, *r);
-      r->have = true;
-    }
+    if (s->groups.size() && (uint64_t)s->qs.size() * s->n_keys >= 0xFFFFFFFFull)
+      throw std::invalid_argument("queries x keys of a batch must stay below 2^32 (job ids are u32)");
+    for (auto& r : s->qs)  // a stream carries NFA state between batches: stencil queries run on the NFA there
+      if (r->group < 0) run_stencil(s, *r);
+    for (auto& g : s->groups) run_nfa(s, *g);
+    for (auto& r : s->qs) r->have = true;
   });
 }
 
@@ -818,10 +961,10 @@ int cep_key_errors(cep_session* s, int query, int32_t* code, uint32_t* seq, uint
     DeviceGuard g(s->device);
     std::vector<KeyState> ks(n_keys);
     if (n_keys)
-      HIPCHECK(hipMemcpyAsync(ks.data(), r.ks.p, sizeof(KeyState) * n_keys, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipMemcpyAsync(ks.data(), r.ks_dev, sizeof(KeyState) * n_keys, hipMemcpyDeviceToHost, s->stream));
     HIPCHECK(hipStreamSynchronize(s->stream));
-    for (uint64_t k = 0; k < n_keys; k++) {
-      if (code) code[k] = ks[k].err;
+    for (uint64_t k = 0; k < n_keys; k++) {  // (a resource limit left after the re-runs: capacity)
+      if (code) code[k] = ks[k].err == KE_RETRY ? KE_CAPACITY : ks[k].err;
       if (seq) seq[k] = ks[k].err_seq;
     }
   });
@@ -1011,6 +1154,21 @@ int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms
   if (kernel_ms) *kernel_ms = s->qs[query]->kernel_ms;
   if (aux_ms) *aux_ms = s->qs[query]->aux_ms;
   if (launches) *launches = s->qs[query]->launches;
+  return CEP_OK;
+}
+
+int cep_last_stats(cep_session* s, int query, cep_batch_stats* out) {
+  if (!s || !out || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  const QueryRt& r = *s->qs[query];
+  if (r.group < 0) {
+    *out = cep_batch_stats{};
+    out->group = 0xFFFFFFFFu;
+    out->kernel_ms = out->main_ms = r.kernel_ms;
+    out->launches = r.launches;
+    return CEP_OK;
+  }
+  *out = s->groups[r.group]->stats;
+  out->group = (uint32_t)r.group;
   return CEP_OK;
 }
 

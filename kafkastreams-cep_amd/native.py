@@ -26,7 +26,8 @@ EXPORTS = [
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
-    "cep_decode_stock_json", "cep_synth_stock_json",
+    "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
+    "cep_last_stats",
 ]
 
 
@@ -38,7 +39,14 @@ class QueryInfo(C.Structure):
 
 class Opts(C.Structure):
     _fields_ = [("device", C.c_int), ("force_nfa", C.c_int), ("tier", C.c_int), ("max_runs", C.c_uint32),
-                ("pool_factor", C.c_double), ("streaming", C.c_int)]
+                ("pool_factor", C.c_double), ("streaming", C.c_int), ("no_groups", C.c_int)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("group", C.c_uint32), ("group_queries", C.c_uint32), ("kernel_ms", C.c_double),
+                ("main_ms", C.c_double), ("retry_ms", C.c_double), ("retried_jobs", C.c_uint64),
+                ("nodes_used", C.c_uint64), ("preds_used", C.c_uint64), ("out_chunks_used", C.c_uint64),
+                ("launches", C.c_uint32)]
 
 
 class Batch(C.Structure):
@@ -72,6 +80,10 @@ def lib():
             "cep_query_destroy": ([vp], None),
             "cep_query_jit_source": ([vp], C.c_char_p),
             "cep_jit_precompile": ([vp, C.POINTER(C.c_double)], C.c_int),
+            "cep_jit_precompile_group": ([C.POINTER(vp), C.c_int, C.POINTER(C.c_double)], C.c_int),
+            "cep_query_group_plan": ([C.POINTER(vp), C.c_int, C.c_int, C.POINTER(C.c_char_p), C.POINTER(u32),
+                                      C.POINTER(C.POINTER(i32)), C.POINTER(u32), C.POINTER(C.POINTER(C.c_int64))],
+                                     C.c_int),
             "cep_session_create": ([C.POINTER(vp), C.c_int, C.POINTER(Opts), C.POINTER(vp)], C.c_int),
             "cep_session_destroy": ([vp], None),
             "cep_push_batch": ([vp, C.POINTER(Batch)], C.c_int),
@@ -83,6 +95,7 @@ def lib():
             "cep_last_timing": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u32)],
                                 C.c_int),
             "cep_last_error": ([], C.c_char_p),
+            "cep_last_stats": ([vp, C.c_int, C.POINTER(BatchStats)], C.c_int),
             "cep_device_alloc": ([C.c_int, C.c_size_t, C.POINTER(vp)], C.c_int),
             "cep_device_free": ([vp], C.c_int),
             "cep_memcpy": ([vp, vp, C.c_size_t, C.c_int, C.c_int], C.c_int),
@@ -141,6 +154,33 @@ class Query:
         if getattr(self, "h", None) and _lib is not None:
             _lib.cep_query_destroy(self.h)
             self.h = None
+
+
+def precompile_group(queries) -> float:
+    """Compile the kernels a session over `queries` launches (one per group of queries that
+    differ only in literals) into the code-object cache, without a GPU; seconds spent."""
+    arr = (C.c_void_p * len(queries))(*[q.h.value for q in queries])
+    t = C.c_double()
+    _check(lib().cep_jit_precompile_group(arr, len(queries), C.byref(t)))
+    return t.value
+
+
+def group_plans(queries) -> list:
+    """The kernel groups a session over `queries` launches: [{members, source, literals}],
+    literals a (members x n) int64 table of the literals that differ (cep_query_group_plan)."""
+    arr = (C.c_void_p * len(queries))(*[q.h.value for q in queries])
+    out = []
+    while True:
+        src, nm, mem, nl, lits = C.c_char_p(), C.c_uint32(), C.POINTER(C.c_int32)(), C.c_uint32(), \
+            C.POINTER(C.c_int64)()
+        rc = lib().cep_query_group_plan(arr, len(queries), len(out), C.byref(src), C.byref(nm), C.byref(mem),
+                                        C.byref(nl), C.byref(lits))
+        if rc != 0:
+            break
+        members = [mem[i] for i in range(nm.value)]
+        table = np.array([lits[i] for i in range(nm.value * nl.value)], np.int64).reshape(nm.value, nl.value)
+        out.append({"members": members, "source": src.value.decode(), "literals": table})
+    return out
 
 
 class DeviceBuffer:
@@ -306,12 +346,14 @@ class Session:
     """cep_session: per-key NFA state for one or more queries on one GPU."""
 
     def __init__(self, queries, device: int = 0, force_nfa: bool = False, max_runs: int = 0,
-                 pool_factor: float = 0.0, tier: int = CEP_TIER_JIT, streaming: bool = False):
+                 pool_factor: float = 0.0, tier: int = CEP_TIER_JIT, streaming: bool = False,
+                 groups: bool = True):
         if isinstance(queries, Query):
             queries = [queries]
         self.queries = list(queries)
         arr = (C.c_void_p * len(self.queries))(*[q.h.value for q in self.queries])
-        opts = Opts(device, 1 if force_nfa else 0, tier, max_runs, pool_factor, 1 if streaming else 0)
+        opts = Opts(device, 1 if force_nfa else 0, tier, max_runs, pool_factor, 1 if streaming else 0,
+                    0 if groups else 1)
         h = C.c_void_p()
         _check(lib().cep_session_create(arr, len(self.queries), C.byref(opts), C.byref(h)))
         self.h = h
@@ -419,6 +461,12 @@ class Session:
         ms, aux, n = C.c_double(), C.c_double(), C.c_uint32()
         _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(aux), C.byref(n)))
         return ms.value, aux.value, n.value
+
+    def stats(self, query: int = 0) -> dict:
+        """cep_last_stats: the last batch's NFA figures for the query's kernel group."""
+        st = BatchStats()
+        _check(lib().cep_last_stats(self.h, query, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in BatchStats._fields_}
 
     def snapshot(self) -> bytes:
         """The streaming session's complete per-key NFA state as a versioned blob

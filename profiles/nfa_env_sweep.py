@@ -32,7 +32,11 @@ def query(name, env, variant):
     for k in KNOBS:
         os.environ.pop(k, None)
     os.environ.update(env)
-    q = N.Query(W.stock_query(variant).to_ir() if variant != "any" else W.any_kleene_query().to_ir())
+    if variant.startswith("mq"):  # one of config 5's variants, e.g. mq63
+        ir = W.multi_queries(64)[int(variant[2:])].to_ir()
+    else:
+        ir = W.stock_query(variant).to_ir() if variant != "any" else W.any_kleene_query().to_ir()
+    q = N.Query(ir)
     for k in KNOBS:
         os.environ.pop(k, None)
     return q
@@ -64,7 +68,7 @@ def main():
         n, d = s.digest(0)
         code, _ = s.key_errors(0)
         res[name] = {"kernel_ms": min(ks), "all_ms": ks, "matches": n, "checksum": f"{d:016x}",
-                     "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2]}
+                     "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2], "stats": s.stats(0)}
         print(name, json.dumps(res[name]), flush=True)
         s.close()
     print(json.dumps(res))

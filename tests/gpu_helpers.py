@@ -7,15 +7,21 @@ from kafkastreams_cep_amd import native as N
 from kafkastreams_cep_amd import workloads as W
 
 
-def gpu_run(ir, key_off, cols, force_nfa=False, ts=None, session=None, tier=N.CEP_TIER_JIT):
+def gpu_run(ir, key_off, cols, force_nfa=False, ts=None, session=None, tier=N.CEP_TIER_JIT, query=0, push=True):
     q = N.Query(ir)
     s = session or N.Session(q, force_nfa=force_nfa, tier=tier)
-    s.push(key_off, cols, ts)
-    m = s.matches(0)
-    code, seq = s.key_errors(0)
+    if push:
+        s.push(key_off, cols, ts)
+    return session_result(s, query, key_off, q.kind)
+
+
+def session_result(s, query, key_off, kind=None):
+    """The last batch's matches and key errors of one query of session `s`, as gpu_run."""
+    m = s.matches(query)
+    code, seq = s.key_errors(query)
     m["err_code"], m["err_seq"] = code, seq
-    m["digest"] = s.digest(0)
-    m["kind"] = q.kind
+    m["digest"] = s.digest(query)
+    m["kind"] = kind
     off = np.asarray(key_off, np.uint64)
     m["emit_pos"] = (off[m["key"].astype(np.int64)] + m["emit_seq"]).astype(np.uint64)
     pair_key = np.repeat(m["key"].astype(np.int64), np.diff(m["pair_off"].astype(np.int64)))

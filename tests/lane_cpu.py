@@ -25,10 +25,11 @@ BUILD = os.path.join(os.environ.get("TMPDIR", "/tmp"), "cep_lane_cpu")
 _libs = {}
 
 
-def build(ir: bytes):
-    """Compile the query's kernel for the host; returns the loaded library (cached)."""
+def build(ir: bytes, source: str | None = None):
+    """Compile the query's kernel (or a group's `source`) for the host; returns the loaded
+    library (cached)."""
     # the occupancy attribute is for the GPU compile only (the host has no kernels)
-    src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\d+\)\)\)", "", N.Query(ir).jit_source)
+    src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\d+\)\)\)", "", source or N.Query(ir).jit_source)
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
                    ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
@@ -44,14 +45,14 @@ def build(ir: bytes):
             f.write(src)
         tmp = so + f".{os.getpid()}"
         subprocess.check_call([CLANG, "-x", "c++", "-std=c++17", "-O1", "-g", "-rdynamic", "-shared", "-fPIC",
-                               "-ffp-contract=off", "-Wno-unused-value", "-w",
+                               "-ffp-contract=off", "-Wno-unused-value", "-w", "-DCEP_LANE_STATS",
                                f"-I{os.path.join(HERE, 'lane_cpu')}", f"-I{CSRC}",
                                f'-DQUERY_SRC="{qsrc}"', os.path.join(HERE, "lane_cpu", "driver.cpp"),
                                "-o", tmp])
         os.replace(tmp, so)
     lib = C.CDLL(so)
     lib.lane_run.argtypes = [C.c_uint64, C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_void_p,
-                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int]
+                             C.c_uint32, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_uint32, C.c_void_p]
     lib.lane_n_matches.restype = C.c_uint64
     lib.lane_n_pairs.restype = C.c_uint64
     lib.lane_fetch.argtypes = [C.c_void_p] * 7
@@ -59,11 +60,13 @@ def build(ir: bytes):
     return lib
 
 
-def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True):
+def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None):
     """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
     the batch continues the keys' streams of the previous streaming call (reset=False).
     bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the chunked scan."""
-    lib = build(ir)
+    lib = build(ir, _group["source"] if _group else None)
+    n_q = len(_group["members"]) if _group else 1
+    kc = np.ascontiguousarray(_group["literals"], np.int64) if _group else None
     if streaming and reset:
         lib.lane_stream_reset()
     key_off = np.ascontiguousarray(key_off, np.uint64)
@@ -72,23 +75,56 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bit
     nk = len(key_off) - 1
     retried = C.c_uint32()
     lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried),
-                 1 if streaming else 0, 1 if bits else 0)
+                 1 if streaming else 0, 1 if bits else 0, n_q, kc.ctypes.data if kc is not None and kc.size else None)
     nm, npairs = lib.lane_n_matches(), lib.lane_n_pairs()
     key = np.zeros(nm, np.uint32)
     emit = np.zeros(nm, np.uint32)
     off = np.zeros(nm + 1, np.uint64)
     seq = np.zeros(npairs, np.uint32)
     stage = np.zeros(npairs, np.uint16)
-    err = np.zeros(nk, np.int32)
-    err_seq = np.zeros(nk, np.uint32)
+    err = np.zeros(nk * n_q, np.int32)
+    err_seq = np.zeros(nk * n_q, np.uint32)
     lib.lane_fetch(*[a.ctypes.data for a in (key, emit, off, seq, stage, err, err_seq)])
     m = {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
          "pair_seq": seq, "pair_stage": stage, "err_code": err, "err_seq": err_seq,
          "retried": retried.value, "bits_used": bool(lib.lane_bits_used())}
+    st = (C.c_uint64 * 8)()
+    lib.lane_stats(st)
+    m["stats"] = dict(zip(("events", "records", "walks", "walk_nodes", "pred_scans", "flushes", "chain_steps",
+                           "flush_iters"), list(st)))
+    if _group:
+        return m
     m["emit_pos"] = (key_off[key.astype(np.int64)] + emit).astype(np.uint64)
     pk = np.repeat(key.astype(np.int64), np.diff(off.astype(np.int64)))
     m["pair_pos"] = (key_off[pk] + seq).astype(np.uint64)
     return m
+
+
+def run_group(irs, key_off, cols, **kw):
+    """The kernel groups a session over `irs` would launch (cep_query_group_plan), each run as
+    one job grid (query, key); returns one result dict per query, as run() would."""
+    key_off = np.ascontiguousarray(key_off, np.uint64)
+    nk = len(key_off) - 1
+    res = [None] * len(irs)
+    for g in N.group_plans([N.Query(ir) for ir in irs]):
+        m = run(irs[g["members"][0]], key_off, cols, _group=g, **kw)
+        job = m["key"].astype(np.int64)
+        lens = np.diff(m["pair_off"].astype(np.int64))
+        for qi, q in enumerate(g["members"]):
+            sel = (job // nk) == qi
+            psel = np.repeat(sel, lens)
+            key = (job[sel] % nk).astype(np.uint32)
+            off = np.zeros(int(sel.sum()) + 1, np.uint64)
+            np.cumsum(lens[sel], out=off[1:])
+            r = {"n_matches": int(sel.sum()), "n_pairs": int(psel.sum()), "key": key, "emit_seq": m["emit_seq"][sel],
+                 "pair_off": off, "pair_seq": m["pair_seq"][psel], "pair_stage": m["pair_stage"][psel],
+                 "err_code": m["err_code"][qi * nk:(qi + 1) * nk], "err_seq": m["err_seq"][qi * nk:(qi + 1) * nk],
+                 "n_group": len(g["members"])}
+            r["emit_pos"] = (key_off[key.astype(np.int64)] + r["emit_seq"]).astype(np.uint64)
+            pk = np.repeat(key.astype(np.int64), lens[sel])
+            r["pair_pos"] = (key_off[pk] + r["pair_seq"]).astype(np.uint64)
+            res[q] = r
+    return res
 
 
 def assert_same(g, r, key_off):

@@ -12,6 +12,8 @@
 #include QUERY_SRC
 
 thread_local LaneDim3 blockIdx, threadIdx, blockDim;
+uint64_t cep_lane_stats[8];
+extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
 
 namespace {
 std::vector<uint32_t> g_key, g_emit, g_seq;
@@ -55,9 +57,10 @@ static bool fill_bits(const A_&, std::vector<uint64_t>&, long) { return false; }
 
 extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const* cols, int n_cols,
                         const int64_t* ts, uint32_t rcap, int defer, uint32_t* n_retried, int streaming,
-                        int use_bits) {
+                        int use_bits, uint32_t n_q, const int64_t* kc) {
   using namespace cep;
   signal(SIGSEGV, on_fault);
+  std::memset(cep_lane_stats, 0, sizeof cep_lane_stats);
   const uint64_t ne = key_off[nk];
   std::vector<Node> nodes_batch, *nodes_p = &nodes_batch;
   std::vector<Pred> preds_batch, *preds_p = &preds_batch;
@@ -77,7 +80,9 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   std::vector<Node>& nodes = *nodes_p;
   std::vector<Pred>& preds = *preds_p;
   std::vector<uint32_t> out((ne + nk * 4 + 64) * 2 * kOutChunkWords);
-  std::vector<KeyState> ks(nk);
+  if (n_q == 0) n_q = 1;
+  const uint64_t jobs = (uint64_t)n_q * nk;
+  std::vector<KeyState> ks(jobs);
   // device pools are not cleared between batches: start from garbage, not zeros
   auto scribble = [](void* p, size_t n) {
     uint64_t x = 0x9E3779B97F4A7C15ull;
@@ -106,6 +111,8 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   a.out_pool = Pool{&out_top, (uint32_t)(out.size() / kOutChunkWords), 1};
   a.ks = ks.data();
   a.n_capacity_err = &n_cap;
+  a.n_q = n_q;
+  a.kc = kc;
   a.n_events = ne;
   std::vector<uint64_t> bits((ne + 63) / 64 + 1, 0);
   g_bits_used = use_bits && fill_bits(a, bits, 0);
@@ -130,23 +137,23 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       cep_nfa_jit(a);
     }
   };
-  launch(nk, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
+  launch(((nk + 63) / 64) * 64 * n_q, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
   *n_retried = 0;
   for (int round = 0; !streaming && n_cap > 0 && round < 3; round++) {  // session.cpp run_nfa
     std::vector<uint32_t> list;
-    for (uint64_t k = 0; k < nk; k++)
-      if (ks[k].err == KE_CAPACITY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
+    for (uint64_t k = 0; k < jobs; k++)
+      if (ks[k].err == KE_RETRY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
     *n_retried += (uint32_t)list.size();
     n_cap = 0;
     rcap *= 8;
-    a.key_list = list.data();
-    a.n_list = (uint32_t)list.size();
+    a.jobs = list.data();
+    a.n_jobs = (uint32_t)list.size();
     launch(list.size(), rcap, 0);
   }
   g_key.clear(); g_emit.clear(); g_seq.clear(); g_off.assign(1, 0); g_stage.clear();
-  g_err.resize(nk); g_err_seq.resize(nk);
-  for (uint64_t k = 0; k < nk; k++) {
-    g_err[k] = ks[k].err;
+  g_err.resize(jobs); g_err_seq.resize(jobs);
+  for (uint64_t k = 0; k < jobs; k++) {  // job k = query k / nk, key k % nk
+    g_err[k] = ks[k].err == KE_RETRY ? KE_CAPACITY : ks[k].err;
     g_err_seq[k] = ks[k].err_seq;
     uint32_t chunk = ks[k].out_first, pos = 0;
     auto next = [&]() -> uint32_t {

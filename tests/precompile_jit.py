@@ -30,6 +30,24 @@ def _irs(bench_only):
     return irs
 
 
+def _group_sets():
+    """query sets whose kernel groups the tests and bench.py launch (cep_jit_precompile_group)"""
+    import cepamd  # noqa: F401
+    from kafkastreams_cep_amd import workloads as W
+
+    mq = W.multi_queries(64)
+    mixed = [W.stock_query("readme", begin_volume=1000), W.any_kleene_query(),
+             W.stock_query("readme", begin_volume=1005), W.stock_query("test"), W.stock_query("readme", dip_num=90)]
+    return [[p.to_ir() for p in mq], [p.to_ir() for p in mq[48:]], [p.to_ir() for p in mixed]]
+
+
+def _compile_group(irs):
+    import cepamd  # noqa: F401
+    from kafkastreams_cep_amd import native as N
+
+    return N.precompile_group([N.Query(ir) for ir in irs])
+
+
 def _compile(ir):
     import cepamd  # noqa: F401
     from kafkastreams_cep_amd import native as N
@@ -45,7 +63,7 @@ def main(bench_only=False, workers=None):
     t = time.time()
     os.environ["CEP_JIT_TOUCH"] = "1"  # cache hits refresh their entry's mtime (jit.cpp)
     with ProcessPoolExecutor(workers or min(8, os.cpu_count() or 1)) as ex:
-        spent = list(ex.map(_compile, irs))
+        spent = list(ex.map(_compile, irs)) + list(ex.map(_compile_group, _group_sets()))
     pruned = 0
     if not bench_only:  # entries no current query maps to (an older kernel source): dropped
         cache = os.path.join(ROOT, "kafkastreams-cep_amd", "jit_cache")

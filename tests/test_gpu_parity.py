@@ -8,7 +8,7 @@ import pytest
 
 import oracle
 from fuzz_queries import random_query, random_stream
-from gpu_helpers import assert_parity, gpu_run
+from gpu_helpers import assert_parity, gpu_run, session_result
 from ref_queries import STOCK_KATS, STRING_KATS, build_case, kats, sequences
 from kafkastreams_cep_amd import native as N
 from kafkastreams_cep_amd import workloads as W
@@ -99,18 +99,54 @@ def test_cfg4_any_kleene_small(tier):
     assert_parity(gpu_run(ir, off, cols, tier=tier), oracle.run(ir, off, cols, threads=8), off)
 
 
-def test_cfg5_multi_query_session():
-    cfg = W.SynthConfig("t", "stock", 500, 600, 0xCE90000 + 5)
+@pytest.mark.parametrize("groups", [True, False])
+def test_cfg5_multi_query_session(groups):
+    """Config 5: all 64 stock-query variants in one session.  With kernel groups they run as
+    ONE launch (lanes = (query, key), literals from the per-query table); without, one launch
+    each.  Every query's matches, event ids, emission order, errors and checksum equal the
+    oracle's (the old test ran 8 queries and compared counts only)."""
+    cfg = W.SynthConfig("t", "stock", 300, 600, 0xCE90000 + 5)
     off, cols = W.generate(cfg)
-    qs = [N.Query(p.to_ir()) for p in W.multi_queries(8)]
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)]
+    s = N.Session(qs, groups=groups)
+    s.push(off, cols)
+    assert s.timing(0)[2] >= 1
+    total = 0
+    for i, q in enumerate(qs):
+        r = oracle.run(q.ir, off, cols, threads=8)
+        total += r["n_matches"]
+        assert_parity(session_result(s, i, off), r, off)
+    assert total > 10000
+
+
+def test_cfg5_group_capacity_retry():
+    """A kernel group whose jobs overflow a 2-record run queue and tiny pools: the jobs that
+    hit a limit are collected on the device and re-run; every query still equals the oracle."""
+    cfg = W.SynthConfig("t", "stock", 200, 500, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)[48:]]
+    s = N.Session(qs, max_runs=2, pool_factor=0.0005)
+    s.push(off, cols)
+    for i, q in enumerate(qs):
+        assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
+    s.push(off, cols)  # pools sized from the first batch's use: same results
+    for i, q in enumerate(qs):
+        assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
+
+
+def test_mixed_session_groups():
+    """Queries of different shapes in one session: stock variants share a group, the
+    any-Kleene query and the zeroOrMore variant run alone, the strict query on the stencil."""
+    cfg = W.SynthConfig("t", "stock", 250, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ps = [W.stock_query("readme", begin_volume=1000), W.any_kleene_query(), W.stock_query("readme", begin_volume=1005),
+          W.stock_query("test"), W.stock_query("readme", dip_num=90)]
+    qs = [N.Query(p.to_ir()) for p in ps]
+    assert [g["members"] for g in N.group_plans(qs)] == [[0, 2, 4], [1], [3]]
     s = N.Session(qs)
     s.push(off, cols)
     for i, q in enumerate(qs):
-        m = s.matches(i)
-        r = oracle.run(q.ir, off, cols, threads=8)
-        assert m["n_matches"] == r["n_matches"]
-        np.testing.assert_array_equal(m["pair_stage"], r["pair_stage"])
-        assert s.digest(i)[0] == r["n_matches"]
+        assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
 
 
 FUZZ_SEEDS = range(0, 160)

@@ -100,3 +100,19 @@ def test_lane_streaming_fuzz(seed):
     outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
     np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
+def test_lane_query_group():
+    """Config 5's 64 stock-query variants as one kernel group (literals from the per-query
+    table, wave W = query W % 64 on 64 keys) against the oracle, query by query; plus a group
+    that hits the capacity retry."""
+    cfg = W.SynthConfig("t", "stock", 70, 500, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    irs = [p.to_ir() for p in W.multi_queries(64)]
+    res = lane_cpu.run_group(irs, off, cols)
+    assert all(r["n_group"] == 64 for r in res)
+    for ir, g in zip(irs, res):
+        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+    small = lane_cpu.run_group(irs[56:64], off, cols, rcap=2)
+    for ir, g in zip(irs[56:64], small):
+        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
