@@ -2,21 +2,27 @@
 """bench.py — events/sec of the README stock Kleene+ query on 1/2/4/8 MI355X.
 
 BASELINE.json metric: "events/sec (whole node) + matches/sec, stock Kleene+ query, 1M keys,
-1/2/4/8 GPU".  One step = one pass of the matcher (libcep.so: cep_nfa_jit + compaction) over
-one batch of 1M keys x ~1000 events per GPU (config 3's shape), inputs already
-resident in HBM, every key starting from the NFA's initial state.  Keys are sharded across
-ranks with no data-path collective (weak scaling: each rank owns its own 1M keys); RCCL only
-all-gathers counts/checksums and reduces the watermark.
+1/2/4/8 GPU" on config 3: 1e9 events over 1M keys.  One step = one pass of the matcher
+(libcep.so: begin-hit bitmap, lane order, cep_nfa_jit, compaction) over one batch, inputs
+already resident in HBM, every key starting from the NFA's initial state.
+
+Multi-GPU: the 1M keys of ONE global stream are sharded by Kafka's
+DefaultPartitioner over the key ids (kafkastreams-cep_amd/shard.py: murmur2 % n_gpus), each
+rank gathering its keys' events on its GPU once before timing; N ranks share the fixed 1e9
+events ("scaling": "strong", BASELINE's config).  --scaling weak gives every rank its own
+1M keys instead.  There is no data-path collective: RCCL only all-gathers the per-rank
+counts/checksums and reduces the watermark (min of the ranks' max event time).
 
     python bench.py                      # N=1, defaults finish in a few minutes
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
-Prints ONE JSON line on rank 0 (contract in the task statement; fields documented in
-DESIGN.md §7).  `roofline` prices cep_nfa_jit at SURVEY §8(d)'s algorithmic bytes (columns read
-once + 4 B per emitted event id + 4 B per match) against 8 TB/s; `cpu_baseline` times the
-oracle (oracle/cep_oracle.cpp, the literal restatement of the reference NFA) on a 1/8 key
-sample on this host's cores.  `ingest` is the JSON decoder (csrc/ingest.hip) on the cfg-3
-stream serialized as StockEvent records, with its own roofline and CPU baseline.
+Prints ONE JSON line on rank 0 (fields documented in DESIGN.md §7).  `roofline` prices
+cep_nfa_jit at SURVEY §8(d)'s algorithmic bytes (columns read once + 4 B per emitted event id +
+4 B per match) against 8 TB/s; `cpu_baseline` times the oracle (oracle/cep_oracle.cpp, the
+literal restatement of the reference NFA) on a 1/8 key sample on this host's cores.  At N=1
+the line also carries config 2 (`secondary`), the arrival-order end-to-end figure, the JSON
+ingest figure and configs 4/5 (`other_configs`), each with key errors, emitted event ids,
+roofline and a CPU baseline.
 """
 import argparse
 import json
@@ -30,10 +36,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import cepamd  # noqa: E402,F401
 from kafkastreams_cep_amd import native as N  # noqa: E402
+from kafkastreams_cep_amd import shard as SH  # noqa: E402
 from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
 METRIC = "events/sec (whole node) + matches/sec, stock Kleene+ query, 1M keys, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+TS_BASE = 1_600_000_000_000  # ts = 1.6e12 + position (ms)
+_T0 = time.time()
+
+
+def log(msg):
+    """progress on stderr (the JSON line alone goes to stdout)"""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 class Dist:
@@ -92,15 +106,16 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def run_steps(sess, stream, steps, warmup, dist):
+def run_steps(sess, stream, steps, warmup, dist, ts=None):
+    tsp = ts.ptr if ts is not None else None
     for _ in range(warmup):
-        sess.push_device(stream)
+        sess.push_device(stream, tsp)
     kern, aux = [], []
     dist.barrier()
     N.lib().cep_sync(sess.h)
     t0 = time.perf_counter()
     for _ in range(steps):
-        sess.push_device(stream)  # returns after the batch's kernels complete
+        sess.push_device(stream, tsp)  # returns after the batch's kernels complete
         k, a, _ = sess.timing(0)
         kern.append(k)
         aux.append(a)
@@ -119,86 +134,191 @@ def load_traffic(name):
         return None
 
 
-def cpu_baseline(cfg, variant, threads, every):
-    """Oracle on keys 0, every, 2*every, ... of the same stream (numpy generator = GPU
-    generator bit for bit).  Also checks GPU == oracle on that sample (checksum)."""
+def roofline(alg_bytes, kernel_ms, kernel, traffic_key=None, **extra):
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": load_traffic(traffic_key or kernel), "kernel": kernel, "kernel_ms": kernel_ms,
+         "algorithmic_bytes": alg_bytes}
+    r.update(extra)
+    return r
+
+
+def match_figures(sess, query, n_keys):
+    """(matches, emitted event ids, keys with an error) of the last batch for one query"""
+    m = N.Matches()
+    N._check(N.lib().cep_poll_matches(sess.h, query, N.CEP_MEM_DEVICE, N.C.byref(m)))
+    code, _ = sess.key_errors(query, n_keys)
+    return int(m.n_matches), int(m.n_pairs), int(np.count_nonzero(code))
+
+
+def global_digest(sess, key_ids):
+    """Checksum of the last batch's matches with GLOBAL key ids (shard key i = key_ids[i]), so
+    the wrapping sum over ranks equals a single GPU's checksum of the whole stream."""
+    m = sess.matches(0)
+    gk = key_ids[m["key"].astype(np.int64)] if key_ids is not None else m["key"]
+    return W.match_digest(gk, m["emit_seq"], m["pair_off"], m["pair_seq"], m["pair_stage"])
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the checker / CPU baseline only
 
+    return oracle
+
+
+def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=False):
+    """The oracle on keys 0, every, 2*every, ... of the same stream (the numpy generator = the
+    GPU generator bit for bit), every query in turn.  events/s = sample events x queries /
+    oracle time.  gpu_check(off, cols) -> per-query (n_matches, checksum) on the GPU for the
+    same sample: the parity spot check."""
+    oracle = _oracle()
     keys = np.arange(0, cfg.n_keys, every)
     off, cols = W.generate(cfg, keys)
-    ir = W.stock_query(variant).to_ir()
-    r = oracle.run(ir, off, cols, threads=threads)
     n_ev = int(off[-1])
-    # parity spot check on the sample: device checksum vs host checksum of the oracle output
-    emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
-    pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
-    pseq = r["pair_pos"].astype(np.uint64) - off[pk]
-    want = (r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]))
-    s = N.Session(N.Query(ir), device=0)
-    s.push(off, cols)
-    got = s.digest(0)
-    s.close()
-    return {"value": n_ev / r["elapsed_s"], "unit": "events/s", "cores": r["threads"], "kind": "port",
-            "sample": f"{len(keys)} of {cfg.n_keys} keys (every {every}th), {n_ev} events, "
-                      f"{r['n_matches']} matches, {r['elapsed_s']:.2f} s on {r['threads']} threads",
-            "matches_per_s": r["n_matches"] / r["elapsed_s"],
-            "parity_on_sample": bool(got == want)}
+    el, n_m, want = 0.0, 0, []
+    for p in queries:
+        r = oracle.run(p.to_ir(), off, cols, threads=threads)
+        el += r["elapsed_s"]
+        n_m += r["n_matches"]
+        emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+        pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+        pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+        want.append((r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"])))
+    out = {"value": n_ev * len(queries) / el, "unit": "events/s" if len(queries) == 1 else "query-events/s",
+           "cores": r["threads"], "kind": "port",
+           "sample": f"{len(keys)} of {cfg.n_keys} keys (every {every}th), {n_ev} events x {len(queries)} "
+                     f"quer{'y' if len(queries) == 1 else 'ies'}, {n_m} matches, {el:.2f} s on {r['threads']} threads"
+                     + (" (rate extrapolated to the full key set)" if extrapolated else ""),
+           "matches_per_s": n_m / el}
+    if gpu_check is not None:
+        out["parity_on_sample"] = bool(gpu_check(off, cols) == want)
+    return out
 
 
-def secondary_strict(device, steps, warmup, dist):
-    """Config 2: strict SEQ(A,B,C), 1e8 events over 1e4 keys, the three stencil passes."""
+def gpu_digests(queries, device):
+    def check(off, cols):
+        qs = [N.Query(p.to_ir()) for p in queries]
+        s = N.Session(qs, device=device)
+        s.push(off, cols)
+        got = [s.digest(i) for i in range(len(qs))]
+        s.close()
+        return got
+    return check
+
+
+def secondary_strict(device, steps, warmup, dist, threads, cpu):
+    """Config 2: strict SEQ(A,B,C), 1e8 events over 1e4 keys, the stencil passes.  CPU
+    baseline: the oracle over the WHOLE stream on all host cores."""
     cfg = W.CONFIGS[2]
     stream = N.synth_stream("abc", cfg.seed, cfg.n_keys, cfg.mean_events, 0, device)
     q = N.Query(W.strict_abc_query().to_ir())
     s = N.Session(q, device=device)
     el, kms, _ = run_steps(s, stream, steps, warmup, dist)
-    n_m, _ = s.digest(0)
+    n_m, dig = s.digest(0)
+    _, n_pairs, n_err = match_figures(s, 0, cfg.n_keys)
     n_ev = stream.n_events
     alg = 4.0 * n_ev + 16.0 * n_m  # one int column + (key + 3 event ids) per match
     res = {"workload": "cfg2: strict SEQ(A,B,C) v<4 | 4<=v<8 | v>=8, 1e4 keys x 1e4 events",
-           "value": n_ev * steps / el, "unit": "events/s", "matches_per_step": n_m,
-           "ms_per_step": 1e3 * el / steps,
-           "roofline": {"bound": "hbm", "achieved": alg / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "traffic": load_traffic("stencil"), "kernel": "stencil_mask+stencil_emit",
-                        "kernel_ms": kms, "algorithmic_bytes": alg}}
+           "value": n_ev * steps / el, "unit": "events/s", "matches_per_step": n_m, "pairs_per_step": n_pairs,
+           "key_errors": n_err, "ms_per_step": 1e3 * el / steps,
+           "roofline": roofline(alg, kms, "stencil_mask+stencil_emit", "stencil")}
     s.close()
+    if cpu:
+        oracle = _oracle()
+        off, cols = stream.download()
+        r = oracle.run(q.ir, off, cols, threads=threads)
+        emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+        pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+        pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+        want = W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"])
+        res["cpu_baseline"] = {"value": n_ev / r["elapsed_s"], "unit": "events/s", "cores": r["threads"],
+                               "kind": "port", "sample": f"the whole stream ({n_ev} events, {r['n_matches']} matches), "
+                                                         f"{r['elapsed_s']:.2f} s on {r['threads']} threads",
+                               "parity_on_sample": bool((r["n_matches"], want) == (n_m, dig))}
     return res
 
 
-def other_configs(device, steps, warmup, dist, keys):
-    """BASELINE configs 4 and 5 on the cfg-3 stream at `keys` keys x ~1000 events on one GPU
-    (parity-tested at reduced size in tests/test_gpu_parity.py): cfg 4 = skip_till_any Kleene+
-    with folds and a 10 ms window, cfg 5 = 64 stock-query variants in one session, which
-    reads the stream once per query launch.  Reported as stream events/s and, for cfg 5,
-    query-events/s (stream events x queries)."""
+def cfg4(device, stream, steps, warmup, dist, threads, cpu_every):
+    """Config 4: skip_till_any Kleene+ with folds and a 10 ms WITHIN over the cfg-3 stream (1M
+    keys): run-explosion / versioned-buffer stress.  Reports buffer nodes per key."""
+    q = N.Query(W.any_kleene_query().to_ir())
+    s = N.Session(q, device=device)
+    el, kms, _ = run_steps(s, stream, steps, warmup, dist)
+    n_m, n_pairs, n_err = match_figures(s, 0, stream.n_keys)
+    st = s.stats(0)
+    s.close()
+    alg = 8.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m
+    res = {"workload": f"cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms, {stream.n_keys} keys x ~1000 "
+                       f"events ({stream.n_events} events) on 1 GPU",
+           "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
+           "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
+           "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
+           "buffer_preds_per_key": st["preds_used"] / max(1, stream.n_keys),
+           "retried_jobs": st["retried_jobs"], "roofline": roofline(alg, kms, "cep_nfa_jit", "cep_nfa_jit_cfg4")}
+    if cpu_every:
+        cfg = W.SynthConfig("cfg4", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
+        res["cpu_baseline"] = cpu_baseline(cfg, [W.any_kleene_query()], threads, cpu_every,
+                                           gpu_digests([W.any_kleene_query()], device), extrapolated=True)
+    return res
+
+
+def cfg5(device, n_keys, sub, steps, warmup, threads, cpu_every):
+    """Config 5: the 64 stock-query variants in ONE session over the cfg-3 stream, 1M keys.  The
+    queries differ only in literals, so libcep runs them as one kernel group (one launch per
+    batch, lanes = (query, key), the columns read once for all 64).  The 1M keys are pushed as
+    key-range batches of `sub` keys (the same stream: the generator is counter-based), so each
+    batch's output (~2.5e9 event ids per 100k keys) stays within HBM; a step = all of them."""
     cfg = W.CONFIGS[3]
-    stream = N.synth_stream("stock", cfg.seed, keys, 1000, 0, device)
-    out = {}
-    for name, queries in (("cfg4", [W.any_kleene_query()]), ("cfg5", W.multi_queries(64))):
-        qs = [N.Query(p.to_ir()) for p in queries]
-        s = N.Session(qs, device=device)
-        el, _, _ = run_steps(s, stream, steps, warmup, dist)
-        kms = [s.timing(i)[0] for i in range(len(qs))]
-        n_m = sum(s.digest(i)[0] for i in range(len(qs)))
-        s.close()
-        ev_s = stream.n_events * steps / el
-        out[name] = {"workload": ("cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms" if name == "cfg4"
-                                  else "cfg5: 64 stock-query variants, one session") +
-                     f", {keys} keys x ~1000 events ({stream.n_events} events) on 1 GPU",
-                     "value": ev_s, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
-                     "queries": len(qs), "query_events_per_s": ev_s * len(qs),
-                     "kernel_ms_sum": float(sum(kms)), "matches_per_step": int(n_m)}
-    return out
+    parts = []
+    for b in range(0, n_keys, sub):
+        parts.append(N.synth_stream("stock", cfg.seed, min(sub, n_keys - b), 1000, b, device))
+    queries = W.multi_queries(64)
+    qs = [N.Query(p.to_ir()) for p in queries]
+    s = N.Session(qs, device=device)
+    tot = {"events": sum(p.n_events for p in parts), "matches": 0, "pairs": 0, "errors": 0, "kernel_ms": 0.0,
+           "retried": 0, "wall": 0.0}
+    for it in range(warmup + steps):
+        timed = it >= warmup
+        for bi, p in enumerate(parts):
+            log(f"cfg5 {'step' if timed else 'warmup'} {it} batch {bi}")
+            t0 = time.perf_counter()
+            s.push_device(p)
+            dt = time.perf_counter() - t0
+            if not timed:
+                continue
+            tot["wall"] += dt
+            st = s.stats(0)
+            tot["kernel_ms"] += st["kernel_ms"]
+            tot["retried"] += st["retried_jobs"]
+            for i in range(len(qs)):
+                n_m, n_p, n_e = match_figures(s, i, p.n_keys)
+                tot["matches"] += n_m
+                tot["pairs"] += n_p
+                tot["errors"] += n_e
+    s.close()
+    ev_s = tot["events"] * steps / tot["wall"]
+    alg = 8.0 * tot["events"] * steps + 4.0 * tot["pairs"] + 4.0 * tot["matches"]
+    res = {"workload": f"cfg5: 64 stock-query variants, one session, one kernel group; {n_keys} keys x ~1000 events "
+                       f"({tot['events']} events) on 1 GPU, pushed as {len(parts)} key-range batches of {sub} keys",
+           "value": ev_s, "unit": "events/s", "query_events_per_s": ev_s * len(qs), "queries": len(qs),
+           "ms_per_step": 1e3 * tot["wall"] / steps, "matches_per_step": tot["matches"] // steps,
+           "pairs_per_step": tot["pairs"] // steps, "key_errors": tot["errors"] // steps,
+           "retried_jobs": tot["retried"], "kernel_ms_per_step": tot["kernel_ms"] / steps,
+           "roofline": roofline(alg, tot["kernel_ms"], "cep_nfa_jit (64-query group)", "cep_nfa_jit_cfg5")}
+    if cpu_every:
+        log("cfg5 cpu baseline")
+        c = W.SynthConfig("cfg5", "stock", n_keys, 1000, cfg.seed)
+        res["cpu_baseline"] = cpu_baseline(c, queries, threads, cpu_every, gpu_digests(queries, device),
+                                           extrapolated=True)
+    return res
 
 
 def end_to_end(args, device, dist):
     """SURVEY §8(d)'s secondary figure: the same cfg-3 workload handed over in arrival order
     (a key id per event, round-robin interleaved), so each step includes the device partition
-    (stable radix sort by key + column gather, csrc/partition.hip) before the NFA."""
+    (csrc/partition.hip) before the NFA."""
     cfg = W.CONFIGS[3]
-    st = N.synth_arrival_stream("stock", cfg.seed, args.keys, args.mean, dist.rank * args.keys, device)
+    st = N.synth_arrival_stream("stock", cfg.seed, args.keys, args.mean, 0, device)
     q = N.Query(W.stock_query(args.variant).to_ir())
     s = N.Session(q, device=device)
     for _ in range(max(1, args.warmup)):
@@ -223,12 +343,13 @@ def end_to_end(args, device, dist):
 
 def ingest(device, steps, keys, cpu_sample):
     """the step before the matcher.  The cfg-3 stream at `keys` keys x ~1000
-    events as StockEvent JSON record values back to back in HBM (json-simple's serialization,
-    StockEventSerDe.java:75-82), decoded by cep_decode_stock_json (csrc/ingest.hip) into the int32
-    price/volume columns the matcher reads.  Timed with HIP events on the launch stream;
-    algorithmic bytes = record text + 8 B offset read + 4+4+4 B (price, volume, status) written
-    per record.  CPU baseline: oracle/json_oracle.py (the json-simple restatement, 1 thread) on
-    the first `cpu_sample` records."""
+    events as StockEvent JSON record values back to back in HBM, in the serializer's own key
+    order (json-simple JSONObject = HashMap: volume, price, name; StockEventSerDe.java:75-82),
+    decoded by cep_decode_stock_json (csrc/ingest.hip) into the int32 price/volume columns the
+    matcher reads.  Timed with HIP events on the launch stream; algorithmic bytes = record text
+    + 8 B offset read + 4+4+4 B (price, volume, status) written per record.  CPU baseline:
+    oracle/json_oracle.py (the json-simple restatement, 1 thread) on the first `cpu_sample`
+    records."""
     import ctypes as C
 
     hip = C.CDLL("libamdhip64.so")
@@ -257,8 +378,8 @@ def ingest(device, steps, keys, cpu_sample):
     alg = batch.nbytes + 8 * (n + 1) + 12 * n
     achieved = alg / (ms * 1e-3) / 1e9
     res = {"workload": f"StockEvent JSON -> int32 columns, cfg3 stream {keys} keys x ~1000 events ({n} records, "
-                       f"{batch.nbytes} bytes)", "value": n / (ms * 1e-3), "unit": "records/s",
-           "ms_per_step": ms, "bytes_per_s": batch.nbytes / (ms * 1e-3), "failed_records": bad,
+                       f"{batch.nbytes} bytes, json-simple key order)", "value": n / (ms * 1e-3),
+           "unit": "records/s", "ms_per_step": ms, "bytes_per_s": batch.nbytes / (ms * 1e-3), "failed_records": bad,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("decode_stock_json_kernel"),
                         "kernel": "decode_stock_json_kernel (+ decode_stock_json_general over pending records)",
@@ -291,8 +412,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--keys", type=int, default=1_000_000, help="keys per GPU")
+    ap.add_argument("--keys", type=int, default=1_000_000, help="keys of the stream (strong) or per GPU (weak)")
     ap.add_argument("--mean", type=int, default=1000, help="mean events per key")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--variant", default="readme", choices=["readme", "test"])
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--cpu-every", type=int, default=8)
@@ -301,35 +423,45 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the arrival-order end-to-end figure")
     ap.add_argument("--no-other", action="store_true", help="skip the cfg 4 / cfg 5 figures")
     ap.add_argument("--no-ingest", action="store_true", help="skip the JSON ingest figure")
-    ap.add_argument("--other-keys", type=int, default=100_000, help="keys of the cfg 4 / cfg 5 figures")
+    ap.add_argument("--ingest-keys", type=int, default=100_000, help="keys of the JSON ingest figure")
+    ap.add_argument("--cfg5-keys", type=int, default=1_000_000)
+    ap.add_argument("--cfg5-batch", type=int, default=125_000, help="keys per pushed batch of config 5")
     args = ap.parse_args()
 
     dist = Dist()
     if dist.world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
     device = dist.local
-    cfg = W.SynthConfig("cfg3_stock", "stock", args.keys, args.mean, W.CONFIGS[3].seed,
-                        key_base=dist.rank * args.keys)
-    stream = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events, cfg.key_base, device)
+    strong = args.scaling == "strong"
+    key_base = 0 if strong else dist.rank * args.keys
+    cfg = W.SynthConfig("cfg3_stock", "stock", args.keys, args.mean, W.CONFIGS[3].seed, key_base=key_base)
+    stream = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events, key_base, device)
+    ts = N.synth_ts(stream.n_events, TS_BASE, device)
+    key_ids = None  # shard key i -> global key id
+    if strong and dist.world > 1:  # this rank's shard of the one global stream (Kafka partitioner)
+        keys, local_off = SH.shard_layout(W.key_offsets(cfg), dist.world, dist.rank)
+        whole, whole_ts = stream, ts
+        stream, ts = N.shard_stream(whole, keys, local_off, whole_ts)
+        del whole, whole_ts
+        key_ids = keys.astype(np.int64)
+    elif not strong:
+        key_ids = np.arange(args.keys, dtype=np.int64) + key_base
     q = N.Query(W.stock_query(args.variant).to_ir())
     sess = N.Session(q, device=device)
-    el, kms, aux_ms = run_steps(sess, stream, args.steps, args.warmup, dist)
-    n_m, digest = sess.digest(0)
-    code, _ = sess.key_errors(0)
-    n_err = int(np.count_nonzero(code))
-    # pairs emitted (event ids): from the flat output of the last step
-    m = N.Matches()
-    N._check(N.lib().cep_poll_matches(sess.h, 0, N.CEP_MEM_DEVICE, N.C.byref(m)))
-    n_pairs = m.n_pairs
+    log(f"cfg3: {stream.n_keys} keys, {stream.n_events} events on rank {dist.rank}")
+    el, kms, aux_ms = run_steps(sess, stream, args.steps, args.warmup, dist, ts)
+    log(f"cfg3: {1e3 * el / args.steps:.2f} ms per step")
+    n_m, n_pairs, n_err = match_figures(sess, 0, stream.n_keys)
+    st = sess.stats(0)
+    digest = global_digest(sess, key_ids)
     wm = dist.min_i64(sess.watermark())
-    per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err)])
-    checksum = dist.sum_u64(digest)  # wrapping sum of the shards' checksums (shard-local key ids)
-    tot_ev, tot_m = per[:, 0].sum(), per[:, 1].sum()
+    per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err), stream.n_keys])
+    checksum = dist.sum_u64(digest)  # wrapping sum of the shards' checksums (global key ids)
+    tot_ev, tot_m, tot_p = per[:, 0].sum(), per[:, 1].sum(), per[:, 2].sum()
     t_max = per[:, 3].max()
 
     if dist.rank == 0:
         alg = 8.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m  # SURVEY §8(d), rank 0's launch
-        achieved = alg / (kms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
             "value": tot_ev * args.steps / t_max,
@@ -340,35 +472,51 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * t_max / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic: SplitMix64 stock random walk (SURVEY §8d), generated in HBM",
+            "data": "synthetic: SplitMix64 stock random walk (SURVEY §8d), generated in HBM; ts = 1.6e12 + position",
             "config": {"workload": f"cfg3 README stock query SEQ(Stock+ a[], Stock b) skip_till_next, "
                                    f"folds avg/volume, WITHIN 1h ({args.variant} variant)",
-                       "keys_per_gpu": args.keys, "events_per_gpu": int(stream.n_events),
-                       "matches_per_gpu_step": int(n_m), "parallelism": f"key-sharded x{dist.world}",
+                       "keys": int(per[:, 6].sum()), "events": int(tot_ev), "keys_per_gpu": [int(x) for x in per[:, 6]],
+                       "matches_per_step": int(tot_m), "pairs_per_step": int(tot_p),
+                       "parallelism": f"key-sharded x{dist.world} (Kafka DefaultPartitioner: murmur2(key) % "
+                                      f"{dist.world})" if strong else f"key ranges x{dist.world}",
                        "key_errors": int(per[:, 5].sum())},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("cep_nfa_jit"),
-                         "kernel": "cep_nfa_jit", "kernel_ms": kms, "compaction_ms": aux_ms,
-                         "algorithmic_bytes": alg},
+            "roofline": roofline(alg, kms, "cep_nfa_jit", compaction_ms=aux_ms,
+                                 bitmap_sort_ms=st["kernel_ms"] - st["main_ms"] - st["retry_ms"],
+                                 main_ms=st["main_ms"]),
             "watermark": wm,
             "checksum": f"{checksum:016x}",
         }
-        if dist.world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.variant, args.cpu_threads, args.cpu_every)
-        if dist.world == 1 and not args.no_secondary:
-            out["secondary"] = secondary_strict(device, args.steps, args.warmup, dist)
-        if dist.world == 1 and not args.no_e2e:
-            sess.close()
+        one = dist.world == 1
+        cpu = one and not args.no_cpu_baseline
+        if cpu:
+            log("cfg3 cpu baseline")
+            out["cpu_baseline"] = cpu_baseline(cfg, [W.stock_query(args.variant)], args.cpu_threads, args.cpu_every,
+                                               gpu_digests([W.stock_query(args.variant)], device))
+        if one and not args.no_other:
+            log("cfg4")
+            ok = max(1, args.steps // 5)
+            out["other_configs"] = {"cfg4": cfg4(device, stream, ok, 1, dist, args.cpu_threads, 64 if cpu else 0)}
+        sess.close()
+        del stream, ts
+        if one and not args.no_secondary:
+            log("cfg2")
+            out["secondary"] = secondary_strict(device, args.steps, args.warmup, dist, args.cpu_threads, cpu)
+        if one and not args.no_e2e:
+            log("end to end")
             out["end_to_end"] = end_to_end(args, device, dist)
-        if dist.world == 1 and not args.no_ingest:
-            out["ingest"] = ingest(device, args.steps, args.other_keys, 0 if args.no_cpu_baseline else 100_000)
-        if dist.world == 1 and not args.no_other:
-            out["other_configs"] = other_configs(device, max(1, args.steps // 2), 1, dist, args.other_keys)
+        if one and not args.no_ingest:
+            log("ingest")
+            out["ingest"] = ingest(device, args.steps, args.ingest_keys, 100_000 if cpu else 0)
+        if one and not args.no_other:
+            out["other_configs"]["cfg5"] = cfg5(device, args.cfg5_keys, args.cfg5_batch, 1, 1, args.cpu_threads,
+                                                256 if cpu else 0)
+        log("done")
         print(json.dumps(out), flush=True)
-    sess.close()
+    else:
+        sess.close()
     dist.close()
 
 

@@ -252,6 +252,15 @@ typedef struct {
 } cep_batch_stats;
 int cep_last_stats(cep_session* s, int query, cep_batch_stats* out);
 
+/* A shard of a device-resident CSR batch (multi-GPU key sharding): the events of the keys
+ * sel_keys[0..n_sel) (indices into src_key_off) gathered into dst columns at dst_key_off
+ * (the shard's own CSR offsets, [n_sel + 1]).  All arrays are device memory except the
+ * pointer arrays and col_bytes (4 or 8 per column); src_ts/dst_ts may be NULL.  Which keys
+ * a rank owns: kafkastreams-cep_amd/shard.py (Kafka's DefaultPartitioner). */
+int cep_gather_keys(int device, uint64_t n_sel, const uint32_t* sel_keys, const uint64_t* src_key_off,
+                    const uint64_t* dst_key_off, int n_cols, const uint32_t* col_bytes,
+                    const void* const* src_cols, void* const* dst_cols, const int64_t* src_ts, int64_t* dst_ts);
+
 const char* cep_last_error(void);
 int cep_alloc_pinned(size_t bytes, void** out);
 int cep_free_pinned(void* p);
@@ -291,6 +300,8 @@ int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_
  * cep_synth_count returns n_events for sizing. */
 int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
                     uint32_t mean_events, uint64_t* n_events);
+/* Timestamps of a synthetic CSR stream in device memory: ts[i] = base + i (CSR position). */
+int cep_synth_ts(int device, uint64_t n_events, int64_t base, int64_t* ts_dev);
 int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
                        uint32_t mean_events, uint64_t* key_off_dev, int32_t* const* cols_dev);
 /* The same stream in arrival order (round robin: ordered by (index within key, key)): the key

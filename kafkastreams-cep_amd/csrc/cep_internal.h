@@ -54,9 +54,11 @@ hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_li
                                 uint32_t* counts, hipStream_t st);
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
+uint64_t scatter_heavy_bytes(uint64_t n_keys);
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
                           const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
-                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals, hipStream_t st);
+                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals, void* heavy_scratch,
+                          hipStream_t st);
 hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, const uint32_t* m_key,
                          const uint32_t* m_emit, const uint64_t* m_off, const uint32_t* p_seq,
                          const uint16_t* p_stage, unsigned long long* out, hipStream_t st);
@@ -71,6 +73,7 @@ hipError_t synth_stock_json(const int32_t* price, const int32_t* volume, uint64_
                             uint64_t* rec_off, uint64_t* total);
 hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, const uint64_t* key_off,
                         int32_t* c0, int32_t* c1, hipStream_t st);
+hipError_t launch_synth_ts(int64_t* ts, uint64_t n, int64_t base, hipStream_t st);
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
 uint64_t synth_hash_host(uint64_t seed, uint64_t key, uint64_t j);
 std::vector<char> jit_code_object(const std::string& src, double* compile_s);
@@ -86,5 +89,8 @@ hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t
 hipError_t csr_to_arrival(const uint64_t* key_off, uint64_t n_keys, uint64_t n, uint64_t max_nk, const int32_t* c0,
                           const int32_t* c1, uint32_t* key_out, int32_t* o0, int32_t* o1, hipStream_t st);
 std::string jit_cache_key(const std::string& src);
+hipError_t gather_keys(uint64_t n_sel, const uint32_t* sel, const uint64_t* src_off, const uint64_t* dst_off,
+                       int nf, const uint32_t* col_bytes, const void* const* src_cols, void* const* dst_cols,
+                       const int64_t* src_ts, int64_t* dst_ts, hipStream_t st);
 
 }  // namespace cep

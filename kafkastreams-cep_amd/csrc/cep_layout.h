@@ -25,8 +25,8 @@ constexpr int kMaxStencil = 8;     // stages of a CEP_KIND_STENCIL query (stenci
 
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
 enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3 };
-// KE_CONFLICT: a deferred walk would have changed what the step saw (nfa_lane.h); internal,
-// the key is re-run with walks in place.  KE_RETRY: a resource of the launch ran out (run
+// KE_CONFLICT: a deferred walk would have changed what the step saw, or one event queued more
+// walks than the queue holds (nfa_lane.h); internal, the key is re-run with walks in place.  KE_RETRY: a resource of the launch ran out (run
 // queue, walk queue, node / predecessor / output pool); internal, the key is re-run with more.
 // KE_CAPACITY: a hard limit (Dewey RLE pairs, stage depth): final.  A KE_RETRY left after the
 // last re-run is reported as KE_CAPACITY.
@@ -99,6 +99,9 @@ struct alignas(16) Node {
   uint32_t lk;         // walks queued when put() last found this node live (deferred walks)
   uint32_t pad;
 };
+
+// pointer ids: kPred0 | node = the node's first-pointer slot (preds0[node]), else the pool
+constexpr uint32_t kPred0 = 0x80000000u;
 
 // ---- predecessor pointer (TimedKeyValue.Pointer): (version, key|null).  Four quads:
 // {prev, next, removed | pairs << 8, Dewey length}, then the Dewey (value, count) pairs,

@@ -88,10 +88,10 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
     const uint32_t o = (uint32_t)(a + skew - (g0 << 4));
     const uint32_t* tw = (const uint32_t*)tile;
     const uint32_t w0 = o >> 2;
-    fast = json::parse_fast(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
+    fast = json::parse_fast_any(P, [tw, w0](uint32_t j) { return tw[w0 + j]; }, o & 3, len);
   } else {
     const uint32_t* words = (const uint32_t*)((uintptr_t)(bytes + a) & ~(uintptr_t)3);
-    fast = json::parse_fast(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3), len);
+    fast = json::parse_fast_any(P, [words](uint32_t j) { return words[j]; }, (uint32_t)((uintptr_t)(bytes + a) & 3), len);
   }
   if (!fast) {
     status[r] = kPending;
@@ -172,13 +172,14 @@ __global__ void __launch_bounds__(256) json_write_kernel(const int32_t* price, c
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   uint64_t p = off[i];
-  p = put_str(out, p, "{\"name\":\"e");
-  p = put_int(out, p, (int64_t)i + 1);
-  p = put_str(out, p, "\",\"price\":");
-  p = put_int(out, p, price[i]);
-  p = put_str(out, p, ",\"volume\":");
+  // json-simple's JSONObject (a HashMap) iterates volume, price, name (StockEventSerDe.java:75-82)
+  p = put_str(out, p, "{\"volume\":");
   p = put_int(out, p, volume[i]);
-  out[p] = '}';
+  p = put_str(out, p, ",\"price\":");
+  p = put_int(out, p, price[i]);
+  p = put_str(out, p, ",\"name\":\"e");
+  p = put_int(out, p, (int64_t)i + 1);
+  p = put_str(out, p, "\"}");
 }
 
 // lengths -> rec_off (inclusive scan into rec_off+1) ; total bytes returned through *total

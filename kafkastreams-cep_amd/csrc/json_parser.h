@@ -301,12 +301,20 @@ __device__ __forceinline__ void parse_words(Parser& P, Word word, uint32_t lead,
   if (!P.done) P.finish();
 }
 
-// Fast path for the serializer's own layout, {"name":"<text without \" or \\>","price":<int>,"volume":<int>}
-// with at most 18 digits per number (StockEventSerDe.java:75-82, the README's records): a straight
-// scan every lane of a wave runs in step.  On success P holds exactly what the state machine
-// would produce for that record; anything else returns false with P untouched and takes the
-// general path.
-template <typename Word>
+// Fast paths for the two fixed layouts of StockEvent records, numbers of at most 18 digits and
+// a name without '"' or '\\':
+//   kLayoutSerializer {"volume":<int>,"price":<int>,"name":"<text>"}  what StockEventSerDe.serialize
+//       writes (StockEventSerDe.java:75-82): json-simple's JSONObject is a HashMap, whose
+//       iteration order for these three keys (default capacity 16) is bucket 0 volume, 6 price,
+//       8 name
+//   kLayoutReadme     {"name":"<text>","price":<int>,"volume":<int>}  the README's console records
+//       (README.md:73-80)
+// A straight scan every lane of a wave runs in step.  On success P holds exactly what the state
+// machine would produce for that record; anything else returns false with P untouched and takes
+// the general path.
+constexpr int kLayoutSerializer = 0, kLayoutReadme = 1;
+
+template <int kLayout, typename Word>
 __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, uint32_t len) {
   if (len < 31) return false;
   uint32_t cj = 0xFFFFFFFFu, cw = 0;
@@ -345,28 +353,38 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
     v = neg ? -(int64_t)m : (int64_t)m;
     return nd >= 1 && nd <= 18;
   };
-  uint32_t i = 0;
-  if (!lit(i, 0x3A22656D616E227Bull, 8) || !lit(i, 0x22, 1)) return false;  // {"name":"
-  const uint32_t n0 = i;
-  for (;;) {  // the name's closing quote: four bytes at a time (SWAR search for '"' or '\\')
-    if (i + 4 <= len) {
-      const uint32_t x = get4(i), q = x ^ 0x22222222u, e = x ^ 0x5C5C5C5Cu;
-      const uint32_t m = ((q - 0x01010101u) & ~q & 0x80808080u) | ((e - 0x01010101u) & ~e & 0x80808080u);
-      if (!m) { i += 4; continue; }
-      i += (uint32_t)__builtin_ctz(m) >> 3;  // the lowest flagged byte is the first real match
-    } else if (i >= len) {
-      return false;
+  // the name's text from i to its closing quote: four bytes at a time (SWAR search for '"' or '\\')
+  auto name = [&](uint32_t& i, uint32_t& n0, uint32_t& nl) -> bool {
+    n0 = i;
+    for (;;) {
+      if (i + 4 <= len) {
+        const uint32_t x = get4(i), q = x ^ 0x22222222u, e = x ^ 0x5C5C5C5Cu;
+        const uint32_t m = ((q - 0x01010101u) & ~q & 0x80808080u) | ((e - 0x01010101u) & ~e & 0x80808080u);
+        if (!m) { i += 4; continue; }
+        i += (uint32_t)__builtin_ctz(m) >> 3;  // the lowest flagged byte is the first real match
+      } else if (i >= len) {
+        return false;
+      }
+      const uint32_t c = byte(i);
+      if (c == '"') break;
+      if (c == '\\') return false;
+      i++;
     }
-    const uint32_t c = byte(i);
-    if (c == '"') break;
-    if (c == '\\') return false;
+    nl = i - n0;
     i++;
-  }
-  const uint32_t nl = i - n0;
-  i++;
+    return true;
+  };
+  uint32_t i = 0, n0 = 0, nl = 0;
   int64_t pv, vv;
-  if (!lit(i, 0x226563697270222Cull, 8) || !lit(i, 0x3A, 1) || !num(i, pv)) return false;  // ,"price":
-  if (!lit(i, 0x656D756C6F76222Cull, 8) || !lit(i, 0x3A22, 2) || !num(i, vv)) return false;  // ,"volume":
+  if (kLayout == kLayoutSerializer) {
+    if (!lit(i, 0x656D756C6F76227Bull, 8) || !lit(i, 0x3A22, 2) || !num(i, vv)) return false;  // {"volume":
+    if (!lit(i, 0x226563697270222Cull, 8) || !lit(i, 0x3A, 1) || !num(i, pv)) return false;    // ,"price":
+    if (!lit(i, 0x3A22656D616E222Cull, 8) || !lit(i, 0x22, 1) || !name(i, n0, nl)) return false;  // ,"name":"
+  } else {
+    if (!lit(i, 0x3A22656D616E227Bull, 8) || !lit(i, 0x22, 1) || !name(i, n0, nl)) return false;  // {"name":"
+    if (!lit(i, 0x226563697270222Cull, 8) || !lit(i, 0x3A, 1) || !num(i, pv)) return false;    // ,"price":
+    if (!lit(i, 0x656D756C6F76222Cull, 8) || !lit(i, 0x3A22, 2) || !num(i, vv)) return false;  // ,"volume":
+  }
   if (i + 1 != len || byte(i) != '}') return false;
   P.kind0 = K_STRING; P.name_off = n0; P.name_len = nl; P.name_esc = false;
   P.kind1 = K_INT; P.val1 = pv; P.kind2 = K_INT; P.val2 = vv;
@@ -374,10 +392,16 @@ __device__ __forceinline__ bool parse_fast(Parser& P, Word word, uint32_t lead, 
   return true;
 }
 
+// either fixed layout (the serializer's first)
+template <typename Word>
+__device__ __forceinline__ bool parse_fast_any(Parser& P, Word word, uint32_t lead, uint32_t len) {
+  return parse_fast<kLayoutSerializer>(P, word, lead, len) || parse_fast<kLayoutReadme>(P, word, lead, len);
+}
+
 // a record: the fast path, else the general state machine
 template <typename Word>
 __device__ __forceinline__ void parse_any(Parser& P, Word word, uint32_t lead, uint32_t len) {
-  if (!parse_fast(P, word, lead, len)) parse_words(P, word, lead, len);
+  if (!parse_fast_any(P, word, lead, len)) parse_words(P, word, lead, len);
 }
 
 // the record at `base` in flat memory

@@ -29,16 +29,20 @@ struct NfaArgs {
   void* walks;               // deferred-walk queues, wcap per slot (nfa_lane.h)
   uint32_t wcap;
   uint32_t defer;            // 1: queue buffer walks and drain them wave-wide; 0: walk in place
-  // Jobs: a job is (query qi of the launch, key), id qi * n_keys + key.  Without a job list,
-  // wave W runs query W % n_q on the keys of ranks (W / n_q) * 64 + lane, rank -> key through
-  // `order` (lane order; null = identity).  A retry pass lists its jobs explicitly.
-  const uint32_t* jobs;      // retry pass: slot i runs job jobs[i]; null = the mapping above
-  uint32_t n_jobs;
+  // Jobs: a job is (query qi of the launch, key), id qi * n_keys + key.  Without a job list, job
+  // index i is query i % n_q on the key of rank i / n_q, rank -> key through `order` (lane
+  // order; null = identity).  A retry pass lists its jobs explicitly.  (Streaming sessions,
+  // job_next null: wave W runs query W % n_q on ranks (W / n_q) * 64 + lane.)
+  const uint32_t* jobs;      // retry pass: job index i is job jobs[i]; null = the mapping above
+  uint64_t n_jobs;           // job indices of the launch (persistent lanes)
   const uint32_t* order;     // key of each rank (longest-first lane order), null = identity
+  uint32_t* job_next;        // persistent lanes (nfa_lane.h run_jobs): next job index to claim;
+                             // null: one job per lane (streaming sessions)
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
   Node* nodes;
-  Pred* preds;
+  Pred* preds;               // the predecessor pool (a node's second and later pointers)
+  Pred* preds0;              // a node's first pointer, one slot per node index
   uint32_t* out;             // output chunks (kOutChunkWords words each)
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;

@@ -329,11 +329,18 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// a key whose output chain is long: scattered by a whole wave (scatter_heavy)
+struct HeavyKey {
+  uint32_t key, pad;
+  uint64_t mo, po;  // its first match / pair index in the flat arrays
+};
+constexpr uint32_t kHeavyPairs = 2048;
+
 __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint64_t n, const uint64_t* bsum_m,
                                                        const uint64_t* bsum_p, const uint32_t* out,
                                                        uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
                                                        uint32_t* p_seq, uint16_t* p_stage,
-                                                       const uint64_t* totals) {
+                                                       const uint64_t* totals, HeavyKey* heavy, uint32_t* n_heavy) {
   __shared__ uint64_t sm[256], sp[256];
   const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t nm = k < n ? ks[k].n_matches : 0, npairs = k < n ? ks[k].n_pairs : 0;
@@ -353,13 +360,34 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
   uint64_t po = bsum_p[blockIdx.x] + sp[threadIdx.x] - npairs;
   if (k == 0) m_off[totals[0]] = totals[1];
   if (nm == 0) return;
-  uint32_t chunk = ks[k].out_first, pos = 0;
+  if (npairs >= kHeavyPairs) {  // a wave per heavy key, next launch
+    heavy[atomicAdd(n_heavy, 1u)] = HeavyKey{(uint32_t)k, 0, mo, po};
+    return;
+  }
+  // The key's chain is read 16 words (four 16-B loads issued together) at a time into this
+  // thread's LDS window: one memory round trip per 16 words instead of one per word (a heavy
+  // key's chain holds millions of words).  Chunks are 1 KiB aligned; word 255 links the next.
+  __shared__ uint32_t win_s[256 * 16];
+  uint32_t* win = win_s + threadIdx.x * 16;
+  uint32_t chunk = ks[k].out_first, pos = 0, wi = 16;
   auto next = [&]() -> uint32_t {
-    if (pos == kOutChunkWords - 1) {
-      chunk = out[(uint64_t)chunk * kOutChunkWords + kOutChunkWords - 1];
+    if (pos == kOutChunkWords - 1) {  // the link is the window's last word
+      chunk = win[15];
       pos = 0;
+      wi = 16;
     }
-    return out[(uint64_t)chunk * kOutChunkWords + pos++];
+    if (wi == 16) {
+      const uint4* src = reinterpret_cast<const uint4*>(out + (uint64_t)chunk * kOutChunkWords + pos);
+      const uint4 a = src[0], b = src[1], c = src[2], d = src[3];
+      uint4* dst = reinterpret_cast<uint4*>(win);
+      dst[0] = a;
+      dst[1] = b;
+      dst[2] = c;
+      dst[3] = d;
+      wi = 0;
+    }
+    pos++;
+    return win[wi++];
   };
   for (uint32_t m = 0; m < nm; m++) {
     const uint32_t emit = next();
@@ -387,6 +415,61 @@ __global__ void __launch_bounds__(256) collect_retry(const KeyState* ks, uint64_
   const int e = ks[i].err;
   if (e == KE_RETRY) cap_list[atomicAdd(counts, 1u)] = (uint32_t)i;
   else if (e == KE_CONFLICT) conf_list[atomicAdd(counts + 1, 1u)] = (uint32_t)i;
+}
+
+// One wave per heavy key: the chain is read a whole 1 KiB chunk per wave load (each lane
+// 16 B), the next chunk's load issued before the current one is parsed; the parse runs
+// wave-uniformly on words broadcast from their lanes, lane 0 storing.
+__global__ void __launch_bounds__(256) scatter_heavy(const KeyState* ks, const HeavyKey* heavy, const uint32_t* n_heavy,
+                                                     const uint32_t* out, uint32_t* m_key, uint32_t* m_emit,
+                                                     uint64_t* m_off, uint32_t* p_seq, uint16_t* p_stage) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nh = *n_heavy;
+  for (uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nh; h += gridDim.x * 4) {
+    const HeavyKey hk = heavy[h];
+    const KeyState st = ks[hk.key];
+    uint64_t mo = hk.mo, po = hk.po;
+    uint64_t words = 2ull * st.n_matches + 2ull * st.n_pairs;  // [emit, np, (seq, stage) x np] per match
+    uint32_t chunk = st.out_first;
+    uint4 cur = reinterpret_cast<const uint4*>(out + (uint64_t)chunk * kOutChunkWords)[lane];
+    int state = 0;  // 0 emit, 1 np, 2 seq, 3 stage
+    uint32_t rem = 0, seq = 0;
+    while (words) {
+      const uint32_t link = __shfl(cur.w, 63, 64);  // word 255
+      const uint32_t here = words > kOutChunkWords - 1 ? kOutChunkWords - 1 : (uint32_t)words;
+      uint4 nxt = cur;
+      if (words > here) nxt = reinterpret_cast<const uint4*>(out + (uint64_t)link * kOutChunkWords)[lane];
+      for (uint32_t i = 0; i < here; i++) {
+        const uint32_t src = i >> 2, c = i & 3;
+        const uint32_t v = c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;
+        const uint32_t w = __shfl(v, src, 64);  // every lane holds the same (c): uniform select
+        if (state == 0) {
+          if (lane == 0) {
+            m_key[mo] = hk.key;
+            m_emit[mo] = w;
+            m_off[mo] = po;
+          }
+          mo++;
+          state = 1;
+        } else if (state == 1) {
+          rem = w;
+          state = rem ? 2 : 0;
+        } else if (state == 2) {
+          seq = w;
+          state = 3;
+        } else {
+          if (lane == 0) {
+            p_seq[po] = seq;
+            p_stage[po] = (uint16_t)w;
+          }
+          po++;
+          state = --rem ? 2 : 0;
+        }
+      }
+      words -= here;
+      cur = nxt;
+    }
+  }
 }
 
 // order-independent checksum of the flat match arrays (tests/gpu_helpers.py, bench.py and
@@ -457,14 +540,23 @@ hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m,
   return hipGetLastError();
 }
 
+uint64_t scatter_heavy_bytes(uint64_t n_keys) { return sizeof(HeavyKey) * (n_keys + 1) + 16; }
+
+// heavy_scratch: scatter_heavy_bytes(n_keys), its first word the heavy-key count (zeroed here)
 hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* bsum_m, const uint64_t* bsum_p,
                           const uint32_t* out, uint32_t* m_key, uint32_t* m_emit, uint64_t* m_off,
-                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals,
+                          uint32_t* p_seq, uint16_t* p_stage, const uint64_t* totals, void* heavy_scratch,
                           hipStream_t st) {
   const uint64_t nb = (n_keys + 255) / 256;
   if (nb == 0) return hipSuccess;
+  uint32_t* n_heavy = static_cast<uint32_t*>(heavy_scratch);
+  HeavyKey* heavy = reinterpret_cast<HeavyKey*>(static_cast<char*>(heavy_scratch) + 16);
+  hipError_t e = hipMemsetAsync(n_heavy, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(scatter_matches, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p, out,
-                     m_key, m_emit, m_off, p_seq, p_stage, totals);
+                     m_key, m_emit, m_off, p_seq, p_stage, totals, heavy, n_heavy);
+  hipLaunchKernelGGL(scatter_heavy, dim3(1024), dim3(256), 0, st, ks, heavy, n_heavy, out, m_key, m_emit, m_off,
+                     p_seq, p_stage);
   return hipGetLastError();
 }
 

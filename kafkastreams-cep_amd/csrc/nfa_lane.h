@@ -85,7 +85,11 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_WALK_FLUSH
 #define CEP_WALK_FLUSH 24
 #endif
+#ifndef CEP_JOB_DRAIN
+#define CEP_JOB_DRAIN 1
+#endif
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
+constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
@@ -305,20 +309,24 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- buffer nodes
+  // A node's first predecessor lives in its own slot of A.preds0 (same index as the node,
+  // pred id kPred0 | node); later ones come from the predecessor pool.  A walk step then
+  // reads the node and its first predecessor with four independent 16-B loads - one memory
+  // round trip per node instead of three (node -> pointer -> its version).
   __device__ __forceinline__ v4u* NQ(uint32_t i, int k) const { return reinterpret_cast<v4u*>(A.nodes + i) + k; }
-  __device__ __forceinline__ v4u* PQ(uint32_t i, int k) const { return reinterpret_cast<v4u*>(A.preds + i) + k; }
+  __device__ __forceinline__ Pred& PR(uint32_t p) const {
+    return (p & kPred0) ? A.preds0[p & ~kPred0] : A.preds[p];
+  }
+  __device__ __forceinline__ v4u* PQ(uint32_t p, int k) const { return reinterpret_cast<v4u*>(&PR(p)) + k; }
 
-  // node (sk, event of the chain); CEP_NONE when absent or deleted.
-  // Pool reads whose result feeds the next address of a loop (chains, predecessor lists,
-  // walks) are written field by field: the same reads as one 16-B vector load were seen
-  // to loop forever on gfx950 (the loop-carried value never advanced); stores stay vectors.
+  // node (sk, event of the chain); CEP_NONE when absent or deleted.  (Pool quads are read as
+  // 16-B vectors; v4u is may_alias, so the field writes of the same bytes stay ordered.)
   __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
     for (uint32_t i = first; i != CEP_NONE;) {
       CEP_STAT(6);
-      const Node& n = A.nodes[i];
-      const uint32_t meta = n.meta, nx = n.same_next;
-      if ((meta & 0xFF) == sk) return (meta & 0x100) ? i : CEP_NONE;
-      i = nx;
+      const v4u q1 = *NQ(i, 1);  // {same_next, meta, lk, -}
+      if ((q1.y & 0xFF) == sk) return (q1.y & 0x100) ? i : CEP_NONE;
+      i = q1.x;
     }
     return CEP_NONE;
   }
@@ -334,14 +342,15 @@ struct Lane {
                             2 * k + 1 < kDeweyPairs ? v.c[2 * k + 1] : 0u};
   }
 
-  // a new node at event j holding one predecessor (prev, v): both written as whole quads
+  // a new node at event j holding one predecessor (prev, v) in its first-pred slot: both
+  // written as whole quads
   __device__ __forceinline__ void new_node(uint32_t sk, uint32_t prev, const Dewey& v) {
     const uint32_t i = pool_take(A.node_pool, ncur, nend);
-    const uint32_t p = i == CEP_NONE ? CEP_NONE : pool_take(A.pred_pool, pcur, pend);
-    if (p == CEP_NONE) {
+    if (i == CEP_NONE) {
       err = KE_RETRY;
       return;
     }
+    const uint32_t p = kPred0 | i;
     write_pred(p, prev, v);
     *NQ(i, 0) = v4u{j, 1u, p, p};
     *NQ(i, 1) = v4u{cur_first, sk | 0x100u | (1u << 16), 0u, 0u};
@@ -358,7 +367,7 @@ struct Lane {
     write_pred(p, prev, v);
     Node& n = A.nodes[node];
     if (n.head == CEP_NONE) n.head = p;
-    else A.preds[n.tail].next = p;
+    else PR(n.tail).next = p;
     n.tail = p;
     n.meta += 1u << 16;
   }
@@ -370,11 +379,9 @@ struct Lane {
       new_node(sk, CEP_NONE, v);
       return;
     }
-    const uint32_t p = pool_take(A.pred_pool, pcur, pend);  // a new TimedKeyValue, one pointer
-    if (p == CEP_NONE) {
-      err = KE_RETRY;
-      return;
-    }
+    // a new TimedKeyValue with one pointer: the node's first-pred slot, rewritten (the node is
+    // of the current event: no queued walk can read its old pointers)
+    const uint32_t p = kPred0 | c;
     write_pred(p, CEP_NONE, v);
     Node& n = A.nodes[c];
     n.refs = 1;
@@ -408,19 +415,38 @@ struct Lane {
   // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92, from the node's list head:
   // the first live pointer whose version the walker is compatible with; its key and version
   // come back in prev / ver
-  __device__ __forceinline__ uint32_t first_compat(uint32_t head, const Dewey& walker, uint32_t& prev, Dewey& ver) {
+  // `pre`/`pre0`/`pre1`: the two first quads of pointer `pre`, already loaded (a walk step's
+  // node's first-pred slot)
+  __device__ __forceinline__ uint32_t first_compat(uint32_t head, const Dewey& walker, uint32_t& prev, Dewey& ver,
+                                                   uint32_t pre = CEP_NONE, v4u pre0 = v4u{0, 0, 0, 0},
+                                                   v4u pre1 = v4u{0, 0, 0, 0}, bool* same = nullptr) {
     for (uint32_t p = head; p != CEP_NONE;) {
       CEP_STAT(4);
-      const Pred& e0 = A.preds[p];
-      const uint32_t fl = e0.flags, nxt = e0.next;
+      v4u e0 = pre0, d1 = pre1;
+      if (p != pre) {  // the pointer and its first Dewey quad, loaded together
+        e0 = *PQ(p, 0);
+        d1 = *PQ(p, 1);
+      }
+      const uint32_t fl = e0.z, nxt = e0.y;
       if (!(fl & 1u)) {
+        // the pointer's version is the walker's own (a run's chain: the common case):
+        // compatible, and the walker keeps its version (*same)
+        const uint32_t en = (fl >> 8) & 0xFF;
+        if (same && en <= 2 && en == walker.n && e0.w == walker.len &&
+            (en < 1 || ((int32_t)d1.x == walker.v[0] && d1.y == walker.c[0])) &&
+            (en < 2 || ((int32_t)d1.z == walker.v[1] && d1.w == walker.c[1]))) {
+          prev = e0.x;
+          *same = true;
+          return p;
+        }
         Dewey e;
-        e.n = (fl >> 8) & 0xFF;
-        e.len = e0.len;
+        e.n = en;
+        e.len = e0.w;
 #pragma unroll
         for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
-          v4u d = {0, 0, 0, 0};
-          if ((uint32_t)(2 * k) < e.n) d = *PQ(p, 1 + k);
+          v4u d = k == 0 ? d1 : v4u{0, 0, 0, 0};
+          if (k > 0 && (uint32_t)(2 * k) < e.n) d = *PQ(p, 1 + k);
+          if (k == 0 && e.n == 0) d = v4u{0, 0, 0, 0};
           e.v[2 * k] = (int32_t)d.x;
           e.c[2 * k] = d.y;
           if (2 * k + 1 < kDeweyPairs) {
@@ -429,7 +455,7 @@ struct Lane {
           }
         }
         if (dw_compatible(walker, e)) {
-          prev = e0.prev;
+          prev = e0.x;
           ver = dw_pin(e);
           return p;
         }
@@ -467,7 +493,7 @@ struct Lane {
       return;
     }
     if (wq_n >= A.wcap) {  // more walks in one event than the queue holds: re-run in place
-      err = KE_RETRY;
+      err = KE_CONFLICT;
       return;
     }
     const Dewey v = dw_pin(v0);
@@ -515,13 +541,16 @@ struct Lane {
     }
     CEP_STAT(3);
     Node& n = A.nodes[s];
-    const uint32_t ev_s = n.event, head = n.head, lk = n.lk;
-    uint32_t meta = n.meta;
+    // the node and its first-pred slot: four independent loads, one round trip
+    const v4u n0 = *NQ(s, 0), n1 = *NQ(s, 1);  // {event, refs, head, tail}, {same_next, meta, lk, -}
+    const v4u f0 = *PQ(kPred0 | s, 0), f1 = *PQ(kPred0 | s, 1);
+    const uint32_t ev_s = n0.x, head = n0.z, lk = n1.z;
+    uint32_t meta = n1.y;
     if (!(meta & 0x100)) {
       walk_fail(KE_NPE, t);
       return false;
     }
-    const int32_t refs = n.refs;
+    const int32_t refs = (int32_t)n0.y;
     int32_t left = 1;
     if (flags & kWalkBranch) {
       n.refs = refs + 1;
@@ -548,14 +577,15 @@ struct Lane {
     }
     uint32_t nx = CEP_NONE;
     Dewey nv;
-    const uint32_t p = first_compat(head, w, nx, nv);
+    bool same = false;
+    const uint32_t p = first_compat(head, w, nx, nv, kPred0 | s, f0, f1, &same);
     if (p == CEP_NONE) return false;
     if (left == 0) {  // removePredecessor(pointer)
-      A.preds[p].flags |= 1u;
+      PR(p).flags |= 1u;
       n.meta = meta - (1u << 16);
     }
     if (nx == CEP_NONE) return false;
-    w = nv;  // a value, not a pointer into the pool
+    if (!same) w = nv;  // a value, not a pointer into the pool
     s = nx;
     return true;
   }
@@ -721,80 +751,228 @@ struct Lane {
     return (rd(half, 0, 0).x & 0x00FFFFFFu) == q.begin_stage;
   }
 
+  // ---------------------------------------------------------------- the job's event loop
+  // tick() runs one step of the loop over the key's events (the quiet skip or one event);
+  // false once the events are over (jj == jn) or the step threw (pa_err).  finish() is the
+  // final drain of the deferred walks, after which err holds the job's outcome: a walk's
+  // exception precedes a step exception queued after it (the reference's order).
+  uint32_t jj = 0, jn = 0;  // next event, end
+  int pa_err = KE_OK;       // an exception of the per-event step (walks queued before it go first)
+  uint32_t pa_seq = 0;
+
+  __device__ __forceinline__ bool tick() {
+    bool known = false;
+    if (q.quiet && A.bhits && only_begin()) {
+      // the next event whose begin predicate holds or throws, 64 positions per word;
+      // event() evaluates the predicate there itself (its exception, in order)
+      uint64_t p = base + jj;
+      uint64_t w = A.bhits[p >> 6] >> (p & 63);
+      while (!w) {
+        jj += 64 - (uint32_t)(p & 63);
+        if (jj >= jn) break;
+        p = base + jj;
+        w = A.bhits[p >> 6];
+      }
+      if (jj >= jn) {
+        jj = jn;
+        return false;
+      }
+      jj += (uint32_t)__builtin_ctzll(w);
+      if (jj >= jn) {
+        jj = jn;
+        return false;
+      }
+    } else if (q.quiet && only_begin()) {
+      const uint32_t lim = (jn - jj > kQuietChunk) ? jj + kQuietChunk : jn;
+      const uint32_t h = q.begin_scan(*this, jj, lim);
+      if (err) {
+        pa_err = err;
+        pa_seq = h;
+        return false;
+      }
+      if (h >= lim) {
+        jj = lim;
+        return jj < jn;
+      }
+      jj = h;
+      known = true;  // the scan already found the begin predicate true
+    }
+    j = jj;
+    if (ev_pos != jj) {
+      q.load_ev(ev, base + jj);
+      ev_pos = jj;
+    }
+    event(known);
+    if (err) {
+      pa_err = err;
+      pa_seq = jj;
+      return false;
+    }
+    jj++;
+    return jj < jn;
+  }
+
+  // the step's exception, after the final drain found nothing earlier (drained: flush() ran)
+  __device__ __forceinline__ void finish_err() {
+    if (!err && pa_err != KE_OK) {
+      err = pa_err;
+      err_seq = pa_seq;
+    }
+  }
+
+  // the whole key in one go (streaming sessions: one key per lane and launch)
   __device__ __forceinline__ void run() {
-    const uint32_t n = j0 + n_ev;
-    uint32_t jj = j0;
-    int pa_err = KE_OK;  // an exception of the per-event step (walks queued before it go first)
-    uint32_t pa_seq = 0;
-    while (jj < n) {
+    jj = j0;
+    jn = j0 + n_ev;
+    pa_err = KE_OK;
+    bool more = jj < jn;
+    while (more) {
       if (A.defer && __any(wq_n >= kWalkFlush)) {
         flush();
         if (err) break;
       }
-      bool known = false;
-      if (q.quiet && A.bhits && only_begin()) {
-        // the next event whose begin predicate holds or throws, 64 positions per word;
-        // event() evaluates the predicate there itself (its exception, in order)
-        uint64_t p = base + jj;
-        uint64_t w = A.bhits[p >> 6] >> (p & 63);
-        while (!w) {
-          jj += 64 - (uint32_t)(p & 63);
-          if (jj >= n) break;
-          p = base + jj;
-          w = A.bhits[p >> 6];
-        }
-        if (jj >= n) {
-          jj = n;
-          continue;
-        }
-        jj += (uint32_t)__builtin_ctzll(w);
-        if (jj >= n) {
-          jj = n;
-          continue;
-        }
-      } else if (q.quiet && only_begin()) {
-        const uint32_t lim = (n - jj > kQuietChunk) ? jj + kQuietChunk : n;
-        const uint32_t h = q.begin_scan(*this, jj, lim);
-        if (err) {
-          pa_err = err;
-          pa_seq = h;
-          break;
-        }
-        if (h >= lim) {
-          jj = lim;
-          continue;
-        }
-        jj = h;
-        known = true;  // the scan already found the begin predicate true
-      }
-      j = jj;
-      if (ev_pos != jj) {
-        q.load_ev(ev, base + jj);
-        ev_pos = jj;
-      }
-      event(known);
-      if (err) {
-        pa_err = err;
-        pa_seq = jj;
-        break;
-      }
-      jj++;
+      more = tick();
     }
     if (pa_err != KE_OK || !err) {
       err = KE_OK;
       flush();  // every lane of the wave together
-      if (!err && pa_err != KE_OK) {
-        err = pa_err;
-        err_seq = pa_seq;
-      }
+      finish_err();
+    }
+  }
+
+  // a fresh job: key `k`'s events of this batch from the NFA's initial state
+  // (NFA.initComputationStates :74-81 — the begin stage, version 1, sequence 1).  The pool
+  // chunks in hand (ncur/nend, pcur/pend) stay with the lane.
+  __device__ __forceinline__ void begin_job(uint32_t k) {
+    key = k;
+    base = A.key_off[k];
+    n_ev = (uint32_t)(A.key_off[k + 1] - base);
+    j0 = 0;
+    j = 0;
+    ev_pos = CEP_NONE;
+    half = 0;
+    count = 0;
+    ocount = 0;
+    bdig = 1;
+    n_final = 0;
+    ochunk = CEP_NONE;
+    opos = 0;
+    cur_first = CEP_NONE;
+    err = KE_OK;
+    err_seq = 0;
+    n_matches = n_pairs = 0;
+    out_first = CEP_NONE;
+    wq_n = 0;
+    opc = 0;
+    wt_last = CEP_NONE;
+    wm0 = wp0 = 0;
+    jj = 0;
+    jn = n_ev;
+    pa_err = KE_OK;
+    pa_seq = 0;
+    if (!kBeginReg) {
+      Dewey v;
+      dw_init(v, 1);
+      half = 1;  // push_rec writes the other half: half 0
+      readd_begin(q.begin_stage, v);
+      half = 0;
+      count = 1;
     }
   }
 };
+
+// job index -> (query, key) job id: explicit (retries) or query-minor over the lane order
+__device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
+  if (A.jobs) return A.jobs[idx];
+  const uint32_t nq = A.n_q ? A.n_q : 1;
+  const uint64_t rank = idx / nq;
+  return (idx % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
+}
+
+// Persistent lanes (per-batch sessions).  The launch has about as many lanes as fit the chip;
+// each lane runs job after job, claiming the next ones from a global counter, so a wave no
+// longer waits for its slowest lane's key before taking new work: the lanes of a wave stay
+// busy until the job list runs dry.  Jobs are claimed in list order - keys by estimated work,
+// longest first (cep_nfa_est), queries interleaved - so the longest jobs start first.  Claims
+// are wave-wide: one atomic per claiming round, the idle lanes taking consecutive jobs.  The
+// deferred walks are drained wave-wide as before, and whenever a lane's job has reached its
+// last event (its final drain); only then is the job's KeyState written.
+template <int F, class Q>
+__device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
+  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  Lane<F, Q> L(A, q);
+  L.rb = reinterpret_cast<v4u*>(A.rings) + (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + lane;
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + lane;
+  if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
+    L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + lane;
+  bool has = false, drained = false;
+  int phase = 0;  // 0 events, 1 final drain pending, 2 done
+  uint64_t job = 0;
+  for (;;) {
+    const uint64_t need = __ballot(!has && !drained);
+    if (need) {
+      const int leader = __ffsll((unsigned long long)need) - 1;
+      uint32_t first = 0;
+      if ((int)lane == leader) first = atomicAdd(A.job_next, (uint32_t)__popcll(need));
+      first = __shfl(first, leader, 64);
+      if (!has && !drained) {
+        const uint64_t idx = first + (uint64_t)__popcll(need & ((1ull << lane) - 1ull));
+        if (idx < A.n_jobs) {
+          job = job_id(A, idx);
+          q.set_query((uint32_t)(job / A.n_keys));
+          L.begin_job((uint32_t)(job % A.n_keys));
+          has = true;
+          phase = L.jn > 0 ? 0 : (A.defer ? 1 : 2);
+        } else {
+          drained = true;
+        }
+      }
+    }
+    if (!__any(has)) break;
+    // drain when a queue is long, when kJobDrain lanes wait for their final drain, or when no
+    // lane has events left to run (the finished lanes' drains batched into one flush)
+    const uint64_t ending = __ballot(has && phase == 1);
+    if (A.defer && (__any(has && L.wq_n >= kWalkFlush) ||
+                    (ending && (__popcll(ending) >= kJobDrain || !__any(has && phase == 0))))) {
+      L.flush();  // every lane of the wave together (lanes without a queue leave at once)
+      if (has && phase == 0 && L.err) phase = 2;  // a walk threw mid-job: the job stops there
+      if (has && phase == 1) {
+        L.finish_err();
+        phase = 2;
+      }
+    }
+    if (has && phase == 0 && !L.tick()) {
+      // the events are over (or a step threw): the remaining walks drain at the next flush
+      L.err = KE_OK;
+      phase = 1;
+      if (!A.defer) {
+        L.finish_err();
+        phase = 2;
+      }
+    }
+    if (has && phase == 2) {
+      KeyState& ks = A.ks[job];
+      ks.n_matches = L.n_matches;
+      ks.n_pairs = L.n_pairs;
+      ks.out_first = L.out_first;
+      ks.err = L.err;
+      ks.err_seq = L.err_seq;
+      if (L.err == KE_RETRY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
+      L.wq_n = 0;
+      has = false;
+    }
+  }
+}
 
 // Driver shared by the AOT and JIT kernels: slot -> key, initial or carried state, the
 // batch's events of the key, KeyState (and KeyCarry for the next batch of a stream).
 template <int F, class Q>
 __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullptr) {
+  if (A.job_next) {  // per-batch sessions: persistent lanes over the job list
+    run_jobs<F>(A, q, lds);
+    return;
+  }
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t job;
   if (A.jobs) {

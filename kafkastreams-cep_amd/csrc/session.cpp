@@ -79,7 +79,7 @@ template <class T> struct HVec {  // host copy of a result array
 // A streaming session's per-query NFA state (cep_opts.streaming): every key's run queue,
 // buffer pools and carried lane state persist from one batch to the next.
 struct StreamState {
-  DBuf rings, nodes, preds, carry, tops;  // tops: {node_top, pred_top} (device)
+  DBuf rings, nodes, preds, preds0, carry, tops;  // tops: {node_top, pred_top} (device)
   uint64_t n_keys = 0, node_cap = 0, pred_cap = 0;
   uint32_t node_used = 0, pred_used = 0;  // pool tops after the last batch
   uint32_t rcap = 0;                      // run-queue slots per key (ring layout)
@@ -145,6 +145,7 @@ struct cep_session {
   cep_opts opts{};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  int cus = 256;  // compute units of the device (persistent-lane grids)
   std::vector<std::unique_ptr<QueryRt>> qs;
   std::vector<std::unique_ptr<GroupRt>> groups;
   // batch (device copies when the batch is host-resident)
@@ -164,7 +165,8 @@ struct cep_session {
   std::vector<uint32_t> h_perm;
   bool layout_host_valid = false;
   // scratch
-  DBuf rings, walks, nodes, preds, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
+  DBuf heavy;  // heavy-key list of the output scatter
+  DBuf rings, walks, nodes, preds, preds0, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
 };
 
 namespace {
@@ -181,6 +183,7 @@ struct DeviceGuard {
 struct Scratch {  // small counters, one allocation
   uint32_t node_top, pred_top, out_top, n_cap_err;
   uint32_t tile_counter, overflow, n_retry_cap, n_retry_conflict;
+  uint32_t job_next, pad2;
   uint64_t totals[2];
   uint64_t total;
   unsigned long long digest;
@@ -278,7 +281,8 @@ hipError_t launch_fn(hipFunction_t fn, NfaArgs& a, uint64_t blocks, hipStream_t 
   return hipModuleLaunchKernel(fn, (uint32_t)blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
-constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;  // pool indices are u32
+constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;   // output chunk ids are u32
+constexpr uint64_t kNodeMax = 0x7FFFFFF0ull;   // node / pointer ids: 31 bits (kPred0 tags a node's slot)
 
 // Runs a kernel group over the batch: the begin-hit bitmap and lane order, the matching
 // launch, re-runs of the jobs that hit a capacity limit or a deferred-walk conflict, and the
@@ -290,7 +294,17 @@ void run_nfa(cep_session* s, GroupRt& g) {
   QueryRt& r0 = *s->qs[g.members[0]];
   uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
   const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.0625;
-  const uint64_t slots = ((nk + 63) / 64) * 64 * Q;  // Q waves per 64-key group
+  const bool streaming = s->opts.streaming != 0;  // (a streaming group holds one query)
+  // Per-batch sessions run persistent lanes (nfa_lane.h run_jobs): a grid of about what the
+  // chip holds at once (3 waves per SIMD), every lane claiming job after job.  Streams keep one
+  // lane per key (their run queues live at the key's slot).
+  const uint64_t resident = (uint64_t)s->cus * 12 * 64;
+  auto grid_for = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident); };
+  // $CEP_NO_PERSIST / $CEP_PERSIST (measurement runs): one lane per job / persistent lanes
+  // (single queries run one lane per key: their longest-first lane order already balances the
+  // waves, and persistent lanes cost cfg 3 ~35 %; groups mix light and heavy queries)
+  const bool persist = !streaming && !std::getenv("CEP_NO_PERSIST") && (Q > 1 || std::getenv("CEP_PERSIST"));
+  const uint64_t slots = !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
@@ -304,10 +318,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
   uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_preds * 3 / 2 + 4096);
   uint64_t out_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q * 2 / kOutChunkWords) + jobs / 64 + 1024,
                                         g.last_out * 3 / 2 + 1024);
-  node_cap = std::min<uint64_t>(node_cap, kPoolMax);
-  pred_cap = std::min<uint64_t>(pred_cap, kPoolMax);
+  node_cap = std::min<uint64_t>(node_cap, kNodeMax);
+  pred_cap = std::min<uint64_t>(pred_cap, kNodeMax);
   out_cap = std::min<uint64_t>(out_cap, kPoolMax);  // chunk ids are u32, word addresses u64
   s->nodes.ensure(sizeof(Node) * node_cap);
+  s->preds0.ensure(sizeof(Pred) * node_cap);
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
@@ -319,7 +334,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
-  const bool streaming = s->opts.streaming != 0;  // (a streaming group holds one query)
   StreamState& S = r0.st;
   if (streaming) {
     if (!S.init) {
@@ -338,15 +352,16 @@ void run_nfa(cep_session* s, GroupRt& g) {
     // a stream cannot re-run a key (its state moved on): size the pools for this batch on top
     // of what the stream already holds, generously (capacity errors would be final)
     const uint64_t add = s->n_events + nk * 2 * nchunk + 4096;
-    const uint64_t nn = std::min<uint64_t>(S.node_used + add, kPoolMax);
-    const uint64_t pn = std::min<uint64_t>(S.pred_used + add, kPoolMax);
+    const uint64_t nn = std::min<uint64_t>(S.node_used + add, kNodeMax);
+    const uint64_t pn = std::min<uint64_t>(S.pred_used + add, kNodeMax);
     if (nn > S.node_cap) {
-      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), kPoolMax);
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), kNodeMax);
       S.nodes.grow_keep(sizeof(Node) * c, sizeof(Node) * S.node_used, s->stream);
+      S.preds0.grow_keep(sizeof(Pred) * c, sizeof(Pred) * S.node_used, s->stream);
       S.node_cap = c;
     }
     if (pn > S.pred_cap) {
-      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(pn, S.pred_cap * 3 / 2), kPoolMax);
+      const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(pn, S.pred_cap * 3 / 2), kNodeMax);
       S.preds.grow_keep(sizeof(Pred) * c, sizeof(Pred) * S.pred_used, s->stream);
       S.pred_cap = c;
     }
@@ -368,6 +383,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
   a.preds = s->preds.as<Pred>();
+  a.preds0 = s->preds0.as<Pred>();
   a.out = s->out.as<uint32_t>();
   a.node_pool = Pool{&sc->node_top, (uint32_t)node_cap, nchunk};
   a.pred_pool = Pool{&sc->pred_top, (uint32_t)pred_cap, pchunk};
@@ -375,11 +391,16 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.ks = g.ks.as<KeyState>();
   a.n_capacity_err = &sc->n_cap_err;
   a.n_events = s->n_events;
+  if (persist) {
+    a.job_next = &sc->job_next;
+    a.n_jobs = jobs;
+  }
   if (streaming) {  // walks in place: a conflict could not be re-run (nfa_lane.h)
     a.defer = 0;
     a.rings = S.rings.p;
     a.nodes = S.nodes.as<Node>();
     a.preds = S.preds.as<Pred>();
+    a.preds0 = S.preds0.as<Pred>();
     a.carry = S.carry.as<KeyCarry>();
     a.node_pool = Pool{S.tops.as<uint32_t>(), (uint32_t)S.node_cap, nchunk};
     a.pred_pool = Pool{S.tops.as<uint32_t>() + 1, (uint32_t)S.pred_cap, pchunk};
@@ -445,10 +466,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
     // grow every pool a job ran out of (indices of the used prefix stay valid)
     const bool node_full = h.node_top >= node_cap - nchunk, pred_full = h.pred_top >= pred_cap - pchunk;
     const bool out_full = h.out_top >= out_cap;
-    const uint64_t nn = node_full ? std::min<uint64_t>(node_cap * 4 + nlist * 64, kPoolMax) : node_cap;
-    const uint64_t pn = pred_full ? std::min<uint64_t>(pred_cap * 4 + nlist * 64, kPoolMax) : pred_cap;
+    const uint64_t nn = node_full ? std::min<uint64_t>(node_cap * 4 + nlist * 64, kNodeMax) : node_cap;
+    const uint64_t pn = pred_full ? std::min<uint64_t>(pred_cap * 4 + nlist * 64, kNodeMax) : pred_cap;
     const uint64_t on = out_full ? std::min<uint64_t>(out_cap * 4 + nlist, kPoolMax) : out_cap;
     s->nodes.grow_keep(sizeof(Node) * nn, sizeof(Node) * std::min<uint64_t>(h.node_top, node_cap), s->stream);
+    s->preds0.grow_keep(sizeof(Pred) * nn, sizeof(Pred) * std::min<uint64_t>(h.node_top, node_cap), s->stream);
     s->preds.grow_keep(sizeof(Pred) * pn, sizeof(Pred) * std::min<uint64_t>(h.pred_top, pred_cap), s->stream);
     s->out.grow_keep(sizeof(uint32_t) * kOutChunkWords * on,
                      sizeof(uint32_t) * kOutChunkWords * std::min<uint64_t>(h.out_top, out_cap), s->stream);
@@ -465,16 +487,18 @@ void run_nfa(cep_session* s, GroupRt& g) {
     out_cap = on;
     a.nodes = s->nodes.as<Node>();
     a.preds = s->preds.as<Pred>();
+    a.preds0 = s->preds0.as<Pred>();
     a.out = s->out.as<uint32_t>();
     a.node_pool.cap = (uint32_t)node_cap;
     a.pred_pool.cap = (uint32_t)pred_cap;
     a.out_pool.cap = (uint32_t)out_cap;
     // a bigger run queue per retried job, its ring kept within 16 GiB
     rcap *= 8;
-    const uint64_t most = std::max<uint64_t>(lens[0], lens[1]);
+    const uint64_t most = grid_for(std::max<uint64_t>(lens[0], lens[1]));
     while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
     a.rcap = rcap;
     s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
+    s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));
     a.rings = s->retry_rings.p;
     a.order = nullptr;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
@@ -483,7 +507,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
       a.defer = k == 0 ? 1 : 0;
       a.jobs = k == 0 ? cap_list : conf_list;
       a.n_jobs = lens[k];
-      HIPCHECK(launch_nfa_tier(g, r0.q, a, lens[k], s->stream));
+      a.job_next = &sc->job_next;  // re-runs always on persistent lanes
+      HIPCHECK(hipMemsetAsync(&sc->job_next, 0, sizeof(uint32_t), s->stream));
+      HIPCHECK(launch_nfa_tier(g, r0.q, a, grid_for(lens[k]), s->stream));
       launches++;
       g.stats.retried_jobs += lens[k];
     }
@@ -524,9 +550,10 @@ void run_nfa(cep_session* s, GroupRt& g) {
     r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));
     r.p_seq.ensure(sizeof(uint32_t) * (tot[1] + 1));
     r.p_stage.ensure(sizeof(uint16_t) * (tot[1] + 1));
+    s->heavy.ensure(scatter_heavy_bytes(nk));
     HIPCHECK(launch_scatter(ks, nk, bm, bp, s->out.as<uint32_t>(), r.m_key.as<uint32_t>(), r.m_emit.as<uint32_t>(),
                             r.m_off.as<uint64_t>(), r.p_seq.as<uint32_t>(), r.p_stage.as<uint16_t>(), sc->totals,
-                            s->stream));
+                            s->heavy.p, s->stream));
     if (nk == 0) HIPCHECK(hipMemsetAsync(r.m_off.p, 0, sizeof(uint64_t), s->stream));
     HIPCHECK(hipEventRecord(s->ev1, s->stream));
     HIPCHECK(hipStreamSynchronize(s->stream));
@@ -663,6 +690,7 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
     DeviceGuard g(s->device);
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIPCHECK(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, s->device));
     HIPCHECK(hipEventCreate(&s->ev0));
     HIPCHECK(hipEventCreate(&s->ev1));
     HIPCHECK(hipEventCreate(&s->ev2));
@@ -1009,7 +1037,7 @@ int cep_watermark(cep_session* s, int64_t* out) {
 // stream exactly (tests/test_gpu_parity.py::test_streaming_snapshot_restore).
 namespace {
 constexpr uint64_t kSnapMagic = 0x31504E5350454300ull;  // "\0CEPSNP1"
-constexpr uint32_t kSnapVersion = 1;
+constexpr uint32_t kSnapVersion = 2;  // 2: a node's first pointer in its own slot (preds0)
 
 uint64_t query_fingerprint(const cep_query* q) {
   uint64_t h = 1469598103934665603ull;
@@ -1034,7 +1062,7 @@ uint64_t snap_size(const cep_session* s) {
     n += sizeof(SnapQueryHdr);
     const StreamState& S = r->st;
     if (S.init)
-      n += sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1) + S.ring_bytes + sizeof(Node) * S.node_used +
+      n += sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1) + S.ring_bytes + (sizeof(Node) + sizeof(Pred)) * S.node_used +
            sizeof(Pred) * S.pred_used;
   }
   return n;
@@ -1073,6 +1101,7 @@ int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size) {
       d2h(S.carry.p, sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1));
       d2h(S.rings.p, S.ring_bytes);
       d2h(S.nodes.p, sizeof(Node) * S.node_used);
+      d2h(S.preds0.p, sizeof(Pred) * S.node_used);
       d2h(S.preds.p, sizeof(Pred) * S.pred_used);
     }
   });
@@ -1108,7 +1137,7 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size) {
       if (h.rcap != rcap || h.F != (uint32_t)r->F || h.ring_bytes != ring_size(r->F, std::max<uint64_t>(h.n_keys, 1), rcap))
         return fail(CEP_E_INVALID, "snapshot taken with other session options (max_runs)");
       const uint64_t n = sizeof(KeyCarry) * std::max<uint64_t>(h.n_keys, 1) + h.ring_bytes +
-                         sizeof(Node) * (uint64_t)h.node_used + sizeof(Pred) * (uint64_t)h.pred_used;
+                         (sizeof(Node) + sizeof(Pred)) * (uint64_t)h.node_used + sizeof(Pred) * (uint64_t)h.pred_used;
       if ((uint64_t)(end - q) < n) return fail(CEP_E_INVALID, "snapshot truncated");
       q += n;
     }
@@ -1137,6 +1166,7 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size) {
       S.node_cap = std::max<uint64_t>(h.node_used, 1);
       S.pred_cap = std::max<uint64_t>(h.pred_used, 1);
       h2d(S.nodes, sizeof(Node) * (uint64_t)h.node_used);
+      h2d(S.preds0, sizeof(Pred) * (uint64_t)h.node_used);
       h2d(S.preds, sizeof(Pred) * (uint64_t)h.pred_used);
       S.node_used = h.node_used;
       S.pred_used = h.pred_used;
@@ -1170,6 +1200,21 @@ int cep_last_stats(cep_session* s, int query, cep_batch_stats* out) {
   *out = s->groups[r.group]->stats;
   out->group = (uint32_t)r.group;
   return CEP_OK;
+}
+
+int cep_gather_keys(int device, uint64_t n_sel, const uint32_t* sel_keys, const uint64_t* src_key_off,
+                    const uint64_t* dst_key_off, int n_cols, const uint32_t* col_bytes,
+                    const void* const* src_cols, void* const* dst_cols, const int64_t* src_ts, int64_t* dst_ts) {
+  if (n_sel && (!sel_keys || !src_key_off || !dst_key_off || (n_cols && (!col_bytes || !src_cols || !dst_cols))))
+    return fail(CEP_E_INVALID, "null argument");
+  if (n_cols < 0 || n_cols > kMaxFields) return fail(CEP_E_INVALID, "1..16 columns");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(gather_keys(n_sel, sel_keys, src_key_off, dst_key_off, n_cols, col_bytes, src_cols, dst_cols, src_ts,
+                         dst_ts, nullptr));
+    HIPCHECK(hipDeviceSynchronize());
+  });
 }
 
 int cep_alloc_pinned(size_t bytes, void** out) {
@@ -1234,6 +1279,16 @@ int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uin
     HIPCHECK(hipMemcpy(key_off_dev, off.data(), sizeof(uint64_t) * (n_keys + 1), hipMemcpyHostToDevice));
     HIPCHECK(launch_synth(kind, seed, n_keys, key_base, key_off_dev, cols_dev[0], kind == 1 ? cols_dev[1] : nullptr,
                           nullptr));
+    HIPCHECK(hipDeviceSynchronize());
+  });
+}
+
+int cep_synth_ts(int device, uint64_t n_events, int64_t base, int64_t* ts_dev) {
+  if (!ts_dev && n_events) return fail(CEP_E_INVALID, "null argument");
+  return guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(launch_synth_ts(ts_dev, n_events, base, nullptr));
     HIPCHECK(hipDeviceSynchronize());
   });
 }

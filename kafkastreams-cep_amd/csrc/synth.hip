@@ -52,6 +52,21 @@ hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_b
   return hipGetLastError();
 }
 
+// event timestamps of a synthetic CSR stream: base + CSR position (each key's events in time
+// order, as the reference's stream time advances per record)
+__global__ void __launch_bounds__(256) ts_kernel(int64_t* ts, uint64_t n, int64_t base) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    ts[i] = base + (int64_t)i;
+}
+
+hipError_t launch_synth_ts(int64_t* ts, uint64_t n, int64_t base, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(ts_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, ts, n, base);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) max_kernel(const int64_t* __restrict__ ts, uint64_t n,
                                                   unsigned long long* out) {
   int64_t m = INT64_MIN;

@@ -27,7 +27,7 @@ EXPORTS = [
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
     "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
-    "cep_last_stats",
+    "cep_last_stats", "cep_gather_keys", "cep_synth_ts",
 ]
 
 
@@ -96,6 +96,9 @@ def lib():
                                 C.c_int),
             "cep_last_error": ([], C.c_char_p),
             "cep_last_stats": ([vp, C.c_int, C.POINTER(BatchStats)], C.c_int),
+            "cep_synth_ts": ([C.c_int, u64, C.c_int64, vp], C.c_int),
+            "cep_gather_keys": ([C.c_int, u64, vp, vp, vp, C.c_int, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp),
+                                 vp, vp], C.c_int),
             "cep_device_alloc": ([C.c_int, C.c_size_t, C.POINTER(vp)], C.c_int),
             "cep_device_free": ([vp], C.c_int),
             "cep_memcpy": ([vp, vp, C.c_size_t, C.c_int, C.c_int], C.c_int),
@@ -249,6 +252,36 @@ def synth_stream(kind: str, seed: int, n_keys: int, mean_events: int, key_base: 
     ptrs = (C.c_void_p * ncols)(*[c.ptr for c in cols])
     _check(lib().cep_synth_generate(device, k, seed, n_keys, key_base, mean_events, off.ptr, ptrs))
     return DeviceStream(n_keys, n.value, off, cols, device)
+
+
+def synth_ts(n_events: int, base: int = 1_600_000_000_000, device: int = 0) -> "DeviceBuffer":
+    """Device timestamps base + CSR position for a synthetic stream (cep_synth_ts)."""
+    b = DeviceBuffer(8 * max(1, n_events), device)
+    _check(lib().cep_synth_ts(device, n_events, base, b.ptr))
+    return b
+
+
+def shard_stream(stream: "DeviceStream", keys: np.ndarray, local_off: np.ndarray, ts: "DeviceBuffer | None" = None):
+    """The shard of a device-resident stream holding keys `keys` (shard.shard_layout), its
+    events gathered on the device (cep_gather_keys).  Returns (DeviceStream, ts DeviceBuffer
+    or None); the shard's key i is the stream's key keys[i]."""
+    keys = np.ascontiguousarray(keys, np.uint32)
+    local_off = np.ascontiguousarray(local_off, np.uint64)
+    n = int(local_off[-1])
+    sel = DeviceBuffer(max(4, keys.nbytes), stream.device)
+    if keys.size:
+        sel.upload(keys)
+    off = DeviceBuffer(local_off.nbytes, stream.device)
+    off.upload(local_off)
+    cols = [DeviceBuffer(4 * max(1, n), stream.device) for _ in stream.cols]
+    nc = len(cols)
+    widths = (C.c_uint32 * nc)(*([4] * nc))
+    src = (C.c_void_p * nc)(*[c.ptr for c in stream.cols])
+    dst = (C.c_void_p * nc)(*[c.ptr for c in cols])
+    dts = DeviceBuffer(8 * max(1, n), stream.device) if ts is not None else None
+    _check(lib().cep_gather_keys(stream.device, len(keys), sel.ptr, stream.key_off.ptr, off.ptr, nc, widths, src, dst,
+                                 ts.ptr if ts is not None else None, dts.ptr if dts is not None else None))
+    return DeviceStream(len(keys), n, off, cols, stream.device), dts
 
 
 class ArrivalStream:

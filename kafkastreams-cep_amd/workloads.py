@@ -129,6 +129,13 @@ def key_counts(cfg: SynthConfig, keys: np.ndarray | None = None) -> np.ndarray:
     return (cfg.mean_events - s + (h % np.uint64(2 * s + 1)).astype(np.int64)).astype(np.int64)
 
 
+def key_offsets(cfg: SynthConfig) -> np.ndarray:
+    """CSR offsets u64[n_keys + 1] of the whole stream (no event values)."""
+    off = np.zeros(cfg.n_keys + 1, np.uint64)
+    np.cumsum(key_counts(cfg), out=off[1:])
+    return off
+
+
 def generate(cfg: SynthConfig, keys: np.ndarray | None = None):
     """Host (numpy) generator for `keys` (default: all).  Returns (key_off u64, columns)."""
     keys = np.arange(cfg.n_keys, dtype=np.int64) if keys is None else np.asarray(keys, np.int64)

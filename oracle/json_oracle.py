@@ -232,7 +232,16 @@ def deserialize(data: bytes, col_width: int = 8):
 
 
 def serialize(name: str, price: int, volume: int) -> bytes:
-    """StockEventSerDe.java:75-82 as the README shows it (README.md:73-80)."""
+    """StockEventSerDe.java:75-82: json-simple's JSONObject is a java.util.HashMap (default
+    capacity 16), so toJSONString writes its entries in bucket order, (h ^ h >>> 16) & 15 of
+    String.hashCode: volume 0, price 6, name 8.  (Derived from json-simple 1.1.1's published
+    source and HashMap's iteration order: parity unpinned; names here need no escaping.)"""
+    return b'{"volume":%d,"price":%d,"name":"%s"}' % (volume, price, name.encode())
+
+
+def readme_record(name: str, price: int, volume: int) -> bytes:
+    """The README's demo input records (README.md:73-80), typed into the console producer in
+    the order name, price, volume."""
     return b'{"name":"%s","price":%d,"volume":%d}' % (name.encode(), price, volume)
 
 

@@ -15,7 +15,7 @@ import cepamd  # noqa: E402,F401
 from kafkastreams_cep_amd import native as N  # noqa: E402
 from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
-KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK")
+KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST")
 DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
 
 
@@ -59,7 +59,10 @@ def main():
     stream = N.synth_stream("stock", cfg.seed, args.keys, cfg.mean_events)
     res = {}
     for name, env in vs:
-        s = N.Session(query(name, env, args.query))
+        qq = query(name, env, args.query)
+        if "CEP_NO_PERSIST" in env:  # read by the session at each batch
+            os.environ["CEP_NO_PERSIST"] = env["CEP_NO_PERSIST"]
+        s = N.Session(qq)
         s.push_device(stream)
         ks = []
         for _ in range(args.steps):
@@ -67,6 +70,7 @@ def main():
             ks.append(s.timing(0)[0])
         n, d = s.digest(0)
         code, _ = s.key_errors(0)
+        os.environ.pop("CEP_NO_PERSIST", None)
         res[name] = {"kernel_ms": min(ks), "all_ms": ks, "matches": n, "checksum": f"{d:016x}",
                      "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2], "stats": s.stats(0)}
         print(name, json.dumps(res[name]), flush=True)

@@ -21,7 +21,7 @@ extern "C" int json_cpu_fast_agrees(const uint8_t* rec, uint32_t len, int* agree
   auto w = [words](uint32_t j) { return words[j]; };
   const uint32_t lead = (uint32_t)((uintptr_t)rec & 3);
   cep::json::Parser F, G;
-  const int fast = cep::json::parse_fast(F, w, lead, len);
+  const int fast = cep::json::parse_fast_any(F, w, lead, len);
   cep::json::parse_words(G, w, lead, len);
   int64_t fp, fv, gp, gv;
   uint32_t fo, fl, go, gl;

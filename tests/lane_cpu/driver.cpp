@@ -33,7 +33,7 @@ static void on_fault(int sig) {  // a lane bug: print where, then die
 // a streaming session's state between lane_run calls (streaming != 0)
 struct Stream {
   std::vector<cep::Node> nodes;
-  std::vector<cep::Pred> preds;
+  std::vector<cep::Pred> preds, preds0;
   std::vector<cep::KeyCarry> carry;
   std::vector<cep::v4u> rings;
   uint32_t node_top = 0, pred_top = 0;
@@ -63,22 +63,26 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   std::memset(cep_lane_stats, 0, sizeof cep_lane_stats);
   const uint64_t ne = key_off[nk];
   std::vector<Node> nodes_batch, *nodes_p = &nodes_batch;
-  std::vector<Pred> preds_batch, *preds_p = &preds_batch;
+  std::vector<Pred> preds_batch, *preds_p = &preds_batch, preds0_batch, *preds0_p = &preds0_batch;
   if (streaming) {  // pools persist; a fixed generous size for the tests' streams
     if (g_stream.carry.empty()) {
       g_stream.carry.assign(nk, KeyCarry{});
       g_stream.nodes.resize(1 << 20);
       g_stream.preds.resize(1 << 20);
+      g_stream.preds0.resize(1 << 20);
       g_stream.rings.resize(ring_bytes(8, nk, rcap) / 16 + 64);
     }
     nodes_p = &g_stream.nodes;
     preds_p = &g_stream.preds;
+    preds0_p = &g_stream.preds0;
   } else {
     nodes_batch.resize(ne * 4 + nk * 64 + 4096);
     preds_batch.resize(ne * 4 + nk * 64 + 4096);
+    preds0_batch.resize(nodes_batch.size());
   }
   std::vector<Node>& nodes = *nodes_p;
   std::vector<Pred>& preds = *preds_p;
+  std::vector<Pred>& preds0 = *preds0_p;
   std::vector<uint32_t> out((ne + nk * 4 + 64) * 2 * kOutChunkWords);
   if (n_q == 0) n_q = 1;
   const uint64_t jobs = (uint64_t)n_q * nk;
@@ -94,9 +98,10 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   if (!streaming) {
     scribble(nodes.data(), nodes.size() * sizeof(Node));
     scribble(preds.data(), preds.size() * sizeof(Pred));
+    scribble(preds0.data(), preds0.size() * sizeof(Pred));
   }
   scribble(out.data(), out.size() * 4);
-  uint32_t node_top = 0, pred_top = 0, out_top = 0, n_cap = 0;
+  uint32_t node_top = 0, pred_top = 0, out_top = 0, n_cap = 0, job_next = 0;
   NfaArgs a{};
   a.n_keys = nk;
   a.key_off = key_off;
@@ -104,6 +109,7 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   a.ts = ts;
   a.nodes = nodes.data();
   a.preds = preds.data();
+  a.preds0 = preds0.data();
   a.out = out.data();
   a.node_pool = Pool{streaming ? &g_stream.node_top : &node_top, (uint32_t)nodes.size(), 16};
   a.pred_pool = Pool{streaming ? &g_stream.pred_top : &pred_top, (uint32_t)preds.size(), 16};
@@ -117,7 +123,14 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   std::vector<uint64_t> bits((ne + 63) / 64 + 1, 0);
   g_bits_used = use_bits && fill_bits(a, bits, 0);
   if (g_bits_used) a.bhits = bits.data();
+  // persistent lanes (session.cpp): one "lane" claims every job in turn; streams: lane per key
   auto launch = [&](uint64_t nslots, uint32_t rc, int df) {
+    if (!streaming) {
+      job_next = 0;
+      a.job_next = &job_next;
+      a.n_jobs = a.jobs ? a.n_jobs : jobs;
+      nslots = 64;
+    }
     std::vector<v4u> rings_batch;
     if (!streaming) {
       rings_batch.resize(ring_bytes(8, nslots, rc) / 16 + 64);
@@ -139,16 +152,22 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   };
   launch(((nk + 63) / 64) * 64 * n_q, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
   *n_retried = 0;
-  for (int round = 0; !streaming && n_cap > 0 && round < 3; round++) {  // session.cpp run_nfa
+  for (int round = 0; !streaming && n_cap > 0 && round < 8; round++) {  // session.cpp run_nfa
     std::vector<uint32_t> list;
     for (uint64_t k = 0; k < jobs; k++)
       if (ks[k].err == KE_RETRY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
     *n_retried += (uint32_t)list.size();
     n_cap = 0;
     rcap *= 8;
-    a.jobs = list.data();
-    a.n_jobs = (uint32_t)list.size();
-    launch(list.size(), rcap, 0);
+    std::vector<uint32_t> cap, conf;  // session.cpp: capacity re-runs keep deferred walks, conflicts walk in place
+    for (uint32_t k : list) (ks[k].err == KE_RETRY ? cap : conf).push_back(k);
+    for (int k = 0; k < 2; k++) {
+      std::vector<uint32_t>& l = k == 0 ? cap : conf;
+      if (l.empty()) continue;
+      a.jobs = l.data();
+      a.n_jobs = (uint32_t)l.size();
+      launch(l.size(), rcap, k == 0 ? (streaming ? 0 : defer) : 0);
+    }
   }
   g_key.clear(); g_emit.clear(); g_seq.clear(); g_off.assign(1, 0); g_stage.clear();
   g_err.resize(jobs); g_err_seq.resize(jobs);

@@ -26,7 +26,14 @@ inline unsigned atomicAdd(unsigned* p, unsigned v) {
   return o;
 }
 inline bool __any(int x) { return x != 0; }  // a wave of one lane
-inline unsigned long long __ballot(int x) { return x != 0; }  // (cep_nfa_bits: built, not run)
+// a wave of one lane: the calling lane's own bit (its lane id is threadIdx.x & 63)
+inline unsigned long long __ballot(int x) { return x ? 1ull << (threadIdx.x & 63) : 0ull; }
+inline int __ffsll(unsigned long long x) { return __builtin_ffsll((long long)x); }
+inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+template <class T>
+inline T __shfl(T v, int, int = 64) {  // a wave of one lane: its own value
+  return v;
+}
 inline double __longlong_as_double(long long x) {
   double d;
   std::memcpy(&d, &x, 8);

@@ -38,7 +38,8 @@ def _group_sets():
     mq = W.multi_queries(64)
     mixed = [W.stock_query("readme", begin_volume=1000), W.any_kleene_query(),
              W.stock_query("readme", begin_volume=1005), W.stock_query("test"), W.stock_query("readme", dip_num=90)]
-    return [[p.to_ir() for p in mq], [p.to_ir() for p in mq[48:]], [p.to_ir() for p in mixed]]
+    return [[p.to_ir() for p in mq], [p.to_ir() for p in mq[48:]], [p.to_ir() for p in mq[60:]],
+            [p.to_ir() for p in mixed]]
 
 
 def _compile_group(irs):

@@ -1,6 +1,8 @@
-"""Multi-rank path on the CPU: bench.py's key sharding (rank r owns keys [r K, (r+1) K) of
-the same generator stream) and its gloo/RCCL reductions (all-gather of counts, wrapping
-checksum sum, min watermark), with the oracle standing in for the per-GPU matcher.
+"""Multi-rank path on the CPU: bench.py's key sharding of ONE global stream (Kafka's
+DefaultPartitioner over the key ids, kafkastreams-cep_amd/shard.py: the real split function
+the bench uses) and its gloo/RCCL reductions (all-gather of counts, wrapping checksum sum over
+global key ids, min watermark), with the oracle standing in for the per-GPU matcher (no GPU
+here; tests/test_gpu_parity.py checks the device gather against shard.gather_host).
 The union of the shards must equal one rank running all keys."""
 import os
 import socket
@@ -11,22 +13,39 @@ import numpy as np
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-K, MEAN = 150, 300
+K, MEAN = 300, 300
 
 
-def _shard_result(rank):
+def _global_stream():
     import cepamd  # noqa: F401
-    import oracle
     from kafkastreams_cep_amd import workloads as W
 
-    cfg = W.SynthConfig("t", "stock", K, MEAN, W.CONFIGS[3].seed, key_base=rank * K)
-    off, cols = W.generate(cfg)
-    ir = W.stock_query("readme").to_ir()
-    r = oracle.run(ir, off, cols, threads=2)
-    emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
-    pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+    cfg = W.SynthConfig("t", "stock", K, MEAN, W.CONFIGS[3].seed)
+    return W.generate(cfg)
+
+
+def _digest(r, off, key_ids):
+    """the oracle result's checksum with global key ids (bench.global_digest's definition)"""
+    from kafkastreams_cep_amd import workloads as W
+
+    k = r["key"].astype(np.int64)
+    emit = r["emit_pos"].astype(np.uint64) - off[k]
+    pk = np.repeat(k, np.diff(r["pair_off"].astype(np.int64)))
     pseq = r["pair_pos"].astype(np.uint64) - off[pk]
-    return int(off[-1]), r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"])
+    return W.match_digest(key_ids[k], emit, r["pair_off"], pseq, r["pair_stage"])
+
+
+def _shard_result(rank, world):
+    import cepamd  # noqa: F401
+    import oracle
+    from kafkastreams_cep_amd import shard as SH
+    from kafkastreams_cep_amd import workloads as W
+
+    off, cols = _global_stream()
+    keys, loff = SH.shard_layout(off, world, rank)
+    lcols = SH.gather_host(off, cols, keys, loff)
+    r = oracle.run(W.stock_query("readme").to_ir(), loff, lcols, threads=2)
+    return int(loff[-1]), r["n_matches"], _digest(r, loff, keys.astype(np.int64)), keys
 
 
 def _worker(rank, world, port, out):
@@ -36,13 +55,14 @@ def _worker(rank, world, port, out):
     import bench
 
     dist = bench.Dist(backend="gloo")
-    n_ev, n_m, dig = _shard_result(rank)
-    per = dist.gather([n_ev, n_m])
+    n_ev, n_m, dig, keys = _shard_result(rank, world)
+    per = dist.gather([n_ev, n_m, len(keys)])
     total = dist.sum_u64(dig)
     wm = dist.min_i64(1000 + rank)
     dist.barrier()
     if rank == 0:
-        np.save(out, np.array([per[:, 0].sum(), per[:, 1].sum(), total >> 32, total & 0xFFFFFFFF, wm], np.int64))
+        np.save(out, np.array([per[:, 0].sum(), per[:, 1].sum(), total >> 32, total & 0xFFFFFFFF, wm,
+                               per[:, 2].sum()], np.int64))
     dist.close()
 
 
@@ -52,25 +72,55 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def test_kafka_partitioner_is_a_partition():
+    sys.path[:0] = [ROOT]
+    import cepamd  # noqa: F401
+    from kafkastreams_cep_amd import shard as SH
+
+    keys = np.arange(100_000, dtype=np.uint32)
+    for n in (1, 2, 4, 8):
+        p = SH.partition_of(keys, n)
+        assert p.min() >= 0 and p.max() < n
+        counts = np.bincount(p, minlength=n)
+        assert counts.min() > 0.9 * len(keys) / n  # murmur2 spreads the keys evenly
+    # Kafka's murmur2 restated a second way (scalar Java int arithmetic) for a few keys
+    def murmur2_scalar(key):
+        data = key.to_bytes(4, "big")
+        m, h = 0x5BD1E995, (0x9747B28C ^ 4) & 0xFFFFFFFF
+        k = data[0] | data[1] << 8 | data[2] << 16 | data[3] << 24
+        k = (k * m) & 0xFFFFFFFF
+        k ^= k >> 24
+        k = (k * m) & 0xFFFFFFFF
+        h = (h * m) & 0xFFFFFFFF
+        h ^= k
+        h ^= h >> 13
+        h = (h * m) & 0xFFFFFFFF
+        h ^= h >> 15
+        return h
+    for key in (0, 1, 2, 255, 256, 65535, 123456789, 2**31 - 1, 2**32 - 1):
+        assert int(SH.murmur2_int_keys([key])[0]) == murmur2_scalar(key)
+
+
 def test_two_rank_sharding_matches_single_rank():
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.npy")
         mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
         got = np.load(out)
-    # the same two shards computed in this process, and one rank owning all 2K keys
-    shards = [_shard_result(r) for r in range(2)]
     import cepamd  # noqa: F401
     import oracle
     from kafkastreams_cep_amd import workloads as W
 
-    cfg = W.SynthConfig("t", "stock", 2 * K, MEAN, W.CONFIGS[3].seed)
-    off, cols = W.generate(cfg)
+    shards = [_shard_result(r, 2) for r in range(2)]
+    off, cols = _global_stream()
     whole = oracle.run(W.stock_query("readme").to_ir(), off, cols, threads=2)
-    assert got[0] == sum(s[0] for s in shards) == int(off[-1])
+    whole_digest = _digest(whole, off, np.arange(K, dtype=np.int64))
+    # every key in exactly one shard, every event in its key's shard
+    assert sorted(np.concatenate([s[3] for s in shards]).tolist()) == list(range(K))
+    assert got[5] == K and got[0] == sum(s[0] for s in shards) == int(off[-1])
+    # the union of the shards' matches is the single rank's: counts and global-key checksum
     assert got[1] == sum(s[1] for s in shards) == whole["n_matches"] > 0
-    assert (int(got[2]) << 32 | int(got[3])) == sum(s[2] for s in shards) % (1 << 64)
+    assert (int(got[2]) << 32 | int(got[3])) == sum(s[2] for s in shards) % (1 << 64) == whole_digest
     assert got[4] == 1000
-    # shard r's matches are exactly the whole run's matches on keys [r K, (r+1) K)
-    n0 = int(np.count_nonzero(whole["key"] < K))
+    n0 = int(np.isin(whole["key"], shards[0][3]).sum())
     assert (n0, whole["n_matches"] - n0) == (shards[0][1], shards[1][1])

@@ -119,6 +119,22 @@ def test_cfg5_multi_query_session(groups):
     assert total > 10000
 
 
+def test_heavy_key_output():
+    """Config 5's heaviest (query, key) job: stream key 39664 under variant q63 emits 1474
+    matches / 615005 event ids (a 400x-the-mean key).  Its output chain is scattered by a
+    whole wave (scatter_heavy); alone and beside light keys, persistent lanes or not."""
+    cfg = W.SynthConfig("t", "stock", 1_000_000, 1000, W.CONFIGS[3].seed)
+    off, cols = W.generate(cfg, np.array([5, 39664, 7, 11]))
+    ir = W.multi_queries(64)[63].to_ir()
+    r = oracle.run(ir, off, cols)
+    assert r["n_pairs"] > 600_000
+    assert_parity(gpu_run(ir, off, cols), r, off)
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)[60:]]  # a group: persistent lanes
+    s = N.Session(qs)
+    s.push(off, cols)
+    assert_parity(session_result(s, 3, off), r, off)
+
+
 def test_cfg5_group_capacity_retry():
     """A kernel group whose jobs overflow a 2-record run queue and tiny pools: the jobs that
     hit a limit are collected on the device and re-run; every query still equals the oracle."""
@@ -222,6 +238,30 @@ def test_device_resident_batch_and_digest():
     r = oracle.run(q.ir, off, cols, threads=8)
     g = gpu_run(q.ir, off, cols)
     assert n == r["n_matches"] and (n, dig) == g["digest"]
+
+
+def test_device_shard_gather():
+    """A rank's shard of a device stream (Kafka partitioner + cep_gather_keys) equals the host
+    split (shard.gather_host), timestamps included, and matches like the oracle on it."""
+    from kafkastreams_cep_amd import shard as SH
+    cfg = W.SynthConfig("t", "stock", 500, 300, 0xCE90000 + 3)
+    d = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events)
+    ts = N.synth_ts(d.n_events, 1000)
+    off, cols = d.download()
+    for world, rank in ((2, 0), (2, 1), (8, 5)):
+        keys, loff = SH.shard_layout(off, world, rank)
+        sh, sts = N.shard_stream(d, keys, loff, ts)
+        o2, c2 = sh.download()
+        np.testing.assert_array_equal(o2, loff)
+        for a, b in zip(c2, SH.gather_host(off, cols, keys, loff)):
+            np.testing.assert_array_equal(a, b)
+        t2 = sts.download(np.int64, sh.n_events)
+        np.testing.assert_array_equal(t2, SH.gather_host(off, [1000 + np.arange(d.n_events)], keys, loff)[0])
+        ir = W.stock_query("readme").to_ir()
+        s = N.Session(N.Query(ir))
+        s.push_device(sh, sts.ptr)
+        assert s.watermark() == int(t2.max())
+        assert_parity(session_result(s, 0, o2), oracle.run(ir, o2, c2), o2)
 
 
 def test_watermark():

@@ -1,6 +1,7 @@
 """CPU checks of the JSON ingest oracle (oracle/json_oracle.py): the README demo records decode
-to the README's values (README.md:73-80, the one reference fixture) and re-serialize to the same
-bytes (StockEventSerDe.java:75-82); the hand-written json-simple cases give their outcomes."""
+to the README's values (README.md:73-80, the one reference fixture) and are the console
+producer's layout; the serializer's own layout (StockEventSerDe.java:75-82, json-simple's HashMap
+order) decodes to the same values; the hand-written json-simple cases give their outcomes."""
 import json_cases as JC
 import pytest
 
@@ -13,7 +14,9 @@ def test_readme_records_decode():
         assert (st, p, v) == (J.OK, price, vol)
         off, ln, esc = span
         name = rec[off:off + ln]
-        assert J.serialize(name.decode(), p, v) == rec and not esc
+        assert J.readme_record(name.decode(), p, v) == rec and not esc
+        ser = J.serialize(name.decode(), p, v)  # what StockEventSerDe.serialize writes
+        assert ser.startswith(b'{"volume":') and J.deserialize(ser)[:3] == (J.OK, price, vol)
 
 
 @pytest.mark.parametrize("rec,code", JC.CASES)
@@ -69,8 +72,11 @@ def test_fast_path_taken_for_serializer_records_and_exact():
         [(1, 2), (-5, 0), (123456789012345678, -999999999999999999), (120, 1010)])] + [r for r, _, _ in JC.README]
     assert all(json_cpu.fast_path(r) == (True, True) for r in canon)
     # 19-digit numbers, escapes, other layouts: general path
+    canon += [J.readme_record("e%d" % i, p, v) for i, (p, v) in enumerate([(1, 2), (-5, 0)])]
+    assert all(json_cpu.fast_path(r) == (True, True) for r in canon)
     for r in (J.serialize("e", 1234567890123456789, 1), b'{"name":"a\\"b","price":1,"volume":2}',
-              b'{"price":1,"volume":2,"name":"a"}', b'{"name":"a","price":1,"volume":2} '):
+              b'{"price":1,"volume":2,"name":"a"}', b'{"name":"a","price":1,"volume":2} ',
+              b'{"volume":2,"price":1,"name":"a"} ', b'{"volume":2,"price":1,"name":"a\\u0041"}'):
         assert json_cpu.fast_path(r)[0] is False
     for r in [c for c, _ in JC.CASES] + JC.fuzz(5, 5000):
         assert json_cpu.fast_path(r)[1], r
