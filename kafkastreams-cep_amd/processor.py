@@ -1,0 +1,326 @@
+"""CEPProcessor: the reference's Kafka Streams processor over libcep.
+
+Mirrors `CEPProcessor<K, V>` (CEPProcessor.java:54-193), `Sequence<K, V>` (Sequence.java:9-75)
+and `Event<K, V>` (Event.java:27-93).  Records enter one at a time through
+`process(key, value)` exactly as in the reference; the matching itself runs on the GPU
+in arrival-order micro-batches (`cep_push_batch` on a streaming session, include/cep.h):
+
+* `process(key, value)` skips a null value (CEPProcessor.java:157) and buffers the record
+  with its context metadata (topic, partition, offset, timestamp - Event.java:31-41);
+* the buffer is flushed when it holds `batch_size` records, on `punctuate()` and on
+  `close()` (the reference's `punctuate`/`close` are empty, :167-175: it matches record by
+  record, this processor matches a batch of records per launch);
+* each flush rebuilds every match as a `Sequence` (stage name -> events, in the walk order of
+  `NFA.matchPattern` / `peek`: final stage first, newest event first) and forwards them with
+  `context.forward(None, sequence)` (:161) in the reference's order: by the arrival of the
+  record that completed them, and in emission order within one record;
+* a key whose NFA threw (the per-key errors of `cep_key_errors`) raises that exception after
+  every match of an earlier record has been forwarded, like the reference's `process()`
+  throwing out of the stream thread; the processor is failed from then on.
+
+One difference is by design: the reference keeps ONE NFA per topic
+partition (CEPProcessor.java:117-134), so records of different keys share runs; this
+processor keeps one NFA per key (a Kafka partition is usually one key's stream in the
+reference's demo, where both give the same matches).
+
+The processor keeps every record it was given (the `Event`s a later match may reference) in
+host memory; `max_keys` bounds the dense key space of the device session.  There is no CPU
+matching path: without libcep.so and a GPU, `init()` raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import expr as X
+from . import native as N
+
+_DTYPES = {X.I32: np.int32, X.I64: np.int64, X.F64: np.float64}
+
+
+# ---- Java exceptions a key's NFA can throw (cep_key_errors codes) -------------------------
+class JavaException(RuntimeError):
+    """An exception the reference's `process()` would have thrown (the key and record that
+    raised it are in `key` / `event`)."""
+
+    def __init__(self, msg, key=None, event=None):
+        super().__init__(msg)
+        self.key, self.event = key, event
+
+
+class NullPointerException(JavaException):
+    pass
+
+
+class IllegalStateException(JavaException):
+    pass
+
+
+class ArithmeticException(JavaException):
+    pass
+
+
+class CapacityError(JavaException):
+    """A hard limit of the GPU engine (Dewey run-length pairs, stage depth); the reference
+    has no such limit, so this is never a parity result."""
+
+
+_EXC = {1: NullPointerException, 2: IllegalStateException, 3: ArithmeticException, 16: CapacityError}
+
+
+# ---- Event / Sequence ---------------------------------------------------------------------
+class Event:
+    """Event.java:27-93: a record and where it came from.  Equality and hash are on
+    (topic, partition, offset) only (:48-61); ordering compares offsets within one
+    topic partition, timestamps across partitions (:78-92)."""
+
+    __slots__ = ("key", "value", "timestamp", "topic", "partition", "offset")
+
+    def __init__(self, key, value, timestamp: int, topic: str, partition: int, offset: int):
+        self.key, self.value, self.timestamp = key, value, int(timestamp)
+        self.topic, self.partition, self.offset = topic, int(partition), int(offset)
+
+    def __eq__(self, o):
+        return isinstance(o, Event) and (self.topic, self.partition, self.offset) == \
+            (o.topic, o.partition, o.offset)
+
+    def __hash__(self):
+        return hash((self.topic, self.partition, self.offset))
+
+    def compare_to(self, o: "Event") -> int:
+        if self.topic != o.topic or self.partition != o.partition:
+            return (self.timestamp > o.timestamp) - (self.timestamp < o.timestamp)
+        return (self.offset > o.offset) - (self.offset < o.offset)
+
+    def __lt__(self, o):
+        return self.compare_to(o) < 0
+
+    def __repr__(self):
+        return (f"Event{{key={self.key}, value={self.value}, timestamp={self.timestamp}, "
+                f"topic='{self.topic}', partition={self.partition}, offset={self.offset}}}")
+
+
+class Sequence:
+    """Sequence.java:9-75: events keyed by stage name, in insertion order (a LinkedHashMap)."""
+
+    def __init__(self, mapping=None):
+        self._seq: dict[str, list[Event]] = dict(mapping or {})
+
+    def add(self, stage: str, event: Event) -> "Sequence":
+        self._seq.setdefault(stage, []).append(event)
+        return self
+
+    def get(self, stage: str):
+        return self._seq.get(stage)
+
+    def as_map(self) -> dict:
+        return self._seq
+
+    asMap = as_map
+
+    def size(self) -> int:
+        return sum(len(v) for v in self._seq.values())
+
+    def __eq__(self, o):
+        # :59-73 - every stage of this one is in `o` with the same number of events and all
+        # of them contained (order-insensitive; one-directional, as in the reference)
+        if self is o:
+            return True
+        if not isinstance(o, Sequence):
+            return False
+        for stage, events in self._seq.items():
+            other = o.get(stage)
+            if other is None or len(events) != len(other) or not all(e in other for e in events):
+                return False
+        return True
+
+    __hash__ = None
+
+    def __repr__(self):
+        return "Sequence(" + ", ".join(f"{k}: {[e.offset for e in v]}" for k, v in self._seq.items()) + ")"
+
+
+# ---- a minimal ProcessorContext -----------------------------------------------------------
+class RecordContext:
+    """The part of Kafka's `ProcessorContext` the processor uses: the current record's
+    topic / partition / offset / timestamp, and `forward(key, value)`.  `send(key, value,
+    timestamp)` plays a record into a processor the way a stream task does (offsets count up
+    per topic partition).  A real host passes its own context with the same members."""
+
+    def __init__(self, topic: str = "topic", partition: int = 0):
+        self._topic, self._partition = topic, partition
+        self._offset, self._timestamp = -1, 0
+        self.forwarded: list = []
+        self.processor = None
+
+    def topic(self):
+        return self._topic
+
+    def partition(self):
+        return self._partition
+
+    def offset(self):
+        return self._offset
+
+    def timestamp(self):
+        return self._timestamp
+
+    def forward(self, key, value):
+        self.forwarded.append((key, value))
+
+    def send(self, key, value, timestamp: int, offset: int | None = None):
+        self._offset = self._offset + 1 if offset is None else int(offset)
+        self._timestamp = int(timestamp)
+        self.processor.process(key, value)
+
+
+# ---- the processor ------------------------------------------------------------------------
+class CEPProcessor:
+    """CEPProcessor.java:54-193 over a streaming libcep session (one NFA per key)."""
+
+    def __init__(self, pattern, in_memory: bool = False, *, batch_size: int = 4096,
+                 max_keys: int = 1 << 16, device: int = 0, session_factory=None):
+        self.pattern = pattern
+        self.in_memory = in_memory  # the reference's store choice; device state is in HBM either way
+        self.batch_size = max(1, int(batch_size))
+        self.max_keys = int(max_keys)
+        self.device = device
+        self.schema = pattern.schema
+        if self.schema is None:
+            raise ValueError("the pattern needs an EventSchema (QueryBuilder(schema))")
+        self.ir = pattern.to_ir()  # interns string literals before any value is encoded
+        self._session_factory = session_factory
+        self.context = None
+        self.session = None
+        self.query = None
+        self._key_ids: dict = {}
+        self._keys: list = []
+        self._events: list[list[Event]] = []  # per key id, in arrival order (sequence number)
+        self._buf_key: list[int] = []
+        self._buf_vals: list[tuple] = []
+        self._buf_ts: list[int] = []
+        self._failed: JavaException | None = None
+
+    # -- Processor API --
+    def init(self, context) -> None:
+        """CEPProcessor.java:84-106: binds the context and creates the device session
+        (the reference creates its stores here and the NFA lazily on the first record)."""
+        self.context = context
+        if isinstance(context, RecordContext):
+            context.processor = self
+        if self._session_factory is not None:
+            self.session = self._session_factory(self.ir)
+        else:
+            self.query = N.Query(self.ir)
+            self.session = N.Session(self.query, device=self.device, streaming=True)
+        self.stage_names = list(getattr(self.session, "stage_names", None) or self.query.stage_names)
+
+    def process(self, key, value) -> None:
+        """CEPProcessor.java:155-163."""
+        if self._failed is not None:
+            raise self._failed
+        if value is None:  # :157
+            return
+        kid = self._key_ids.get(key)
+        if kid is None:
+            if len(self._keys) >= self.max_keys:
+                raise ValueError(f"more than max_keys={self.max_keys} distinct keys")
+            kid = self._key_ids[key] = len(self._keys)
+            self._keys.append(key)
+            self._events.append([])
+        ctx = self.context
+        ev = Event(key, value, ctx.timestamp(), ctx.topic(), ctx.partition(), ctx.offset())
+        self._events[kid].append(ev)
+        self._buf_key.append(kid)
+        self._buf_vals.append(self._columns_of(value))
+        self._buf_ts.append(ev.timestamp)
+        if len(self._buf_key) >= self.batch_size:
+            self.flush()
+
+    def punctuate(self, timestamp: int) -> None:
+        """CEPProcessor.java:167-169 (empty there): forwards what is buffered."""
+        self.flush()
+
+    def close(self) -> None:
+        """CEPProcessor.java:172-175: forwards what is buffered and frees the session."""
+        try:
+            if self.session is not None and self._failed is None:
+                self.flush()
+        finally:
+            if self.session is not None and hasattr(self.session, "close"):
+                self.session.close()
+            self.session = None
+
+    # -- batching --
+    def _columns_of(self, value) -> tuple:
+        S = self.schema
+        if S.string_value:
+            return (S.encode_literal(value),)
+        if isinstance(value, dict):
+            return tuple(value[n] for n in S.names)
+        return tuple(getattr(value, n) for n in S.names)
+
+    def flush(self) -> None:
+        """Matches the buffered records on the device and forwards the new Sequences."""
+        if self._failed is not None:
+            raise self._failed
+        n = len(self._buf_key)
+        if n == 0:
+            return
+        keys = np.asarray(self._buf_key, np.uint32)
+        vals = self._buf_vals
+        cols = [np.asarray([v[f] for v in vals], dtype=_DTYPES[t]) for f, t in enumerate(self.schema.types)]
+        ts = np.asarray(self._buf_ts, np.int64)
+        self._buf_key, self._buf_vals, self._buf_ts = [], [], []
+        # per key: the sequence number of its first record in this batch, and the arrival
+        # index of each of its records (a stable partition of the batch by key)
+        counts = np.bincount(keys, minlength=len(self._keys)).astype(np.int64)
+        total = np.asarray([len(e) for e in self._events], np.int64)
+        before = total - counts
+        by_key = np.argsort(keys, kind="stable")
+        start = np.zeros(len(self._keys) + 1, np.int64)
+        np.cumsum(counts, out=start[1:])
+
+        self.session.push_arrival(keys, cols, self.max_keys, ts)
+        m = self.session.matches(0)
+        code, err_seq = self.session.key_errors(0, self.max_keys)
+
+        def arrival(k, seq):
+            return by_key[start[k] + (np.asarray(seq, np.int64) - before[k])]
+
+        # the first record (in arrival order) whose key threw in this batch
+        fail_at, fail_key = n, -1
+        for k in np.flatnonzero(code[:len(self._keys)]):
+            s = int(err_seq[k])
+            if s >= before[k] and s < total[k]:
+                a = int(arrival(k, s))
+                if a < fail_at:
+                    fail_at, fail_key = a, int(k)
+            elif s < before[k]:  # (sticky errors are raised when they first appear)
+                raise RuntimeError("key error from an earlier batch was not raised")
+
+        nm = int(m["n_matches"])
+        if nm:
+            mk = m["key"].astype(np.int64)
+            emit = by_key[start[mk] + (m["emit_seq"].astype(np.int64) - before[mk])]
+            order = np.argsort(emit, kind="stable")
+            off = m["pair_off"].astype(np.int64)
+            pseq = m["pair_seq"].astype(np.int64)
+            pst = m["pair_stage"]
+            names = self.stage_names
+            fwd = self.context.forward
+            for i in order.tolist():
+                if emit[i] >= fail_at:
+                    break
+                evs = self._events[mk[i]]
+                seq = Sequence()
+                for p in range(off[i], off[i + 1]):
+                    seq.add(names[pst[p]], evs[pseq[p]])
+                fwd(None, seq)
+        if fail_key >= 0:
+            c = int(code[fail_key])
+            ev = self._events[fail_key][int(err_seq[fail_key])]
+            exc = _EXC.get(c, JavaException)
+            self._failed = exc(f"{exc.__name__} in the NFA of key {self._keys[fail_key]!r} at "
+                               f"offset {ev.offset} (cep_key_errors code {c})",
+                               key=self._keys[fail_key], event=ev)
+            raise self._failed

@@ -26,6 +26,8 @@ def _irs(bench_only):
         if name in STRING_KATS:
             irs.append(build_case(name, case)[0].to_ir())
     from test_gpu_parity import FUZZ_JIT_SEEDS  # the interpreter-tier seeds need no JIT kernel
+    from test_processor import arith_query
+    irs.append(arith_query().to_ir())
     irs += [random_query(s).to_ir() for s in FUZZ_JIT_SEEDS]
     return irs
 

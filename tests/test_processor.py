@@ -1,0 +1,235 @@
+"""CEPProcessor (kafkastreams_cep_amd/processor.py) against the reference's processor behaviour.
+
+* README.md:73-96: the demo's eight records give exactly the four JSON lines the README
+  prints, after the demo's own rendering (test:demo/CEPStockKStreamsDemo.java:60-71: stage
+  lists reversed to oldest-first, stages in json-simple HashMap order);
+* a many-key interleaved stream forwards the same Sequences in the same order as one
+  reference NFA per key run record by record (the oracle), whatever the batch size;
+* null values are skipped (CEPProcessor.java:157);
+* a key that throws raises that exception after every match of an earlier record was
+  forwarded and none of a later one, and the processor stays failed.
+
+The CPU tests run the processor's host logic over an oracle-backed stand-in for the device
+session (tests/proc_fake.py); the `gpu` tests run the same cases through libcep.so.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle
+from kafkastreams_cep_amd import QueryBuilder
+from kafkastreams_cep_amd import native as N
+from kafkastreams_cep_amd import processor as P
+from kafkastreams_cep_amd import workloads as W
+from proc_fake import OracleStreamSession
+
+README_EVENTS = [("e1", 100, 1010), ("e2", 120, 990), ("e3", 120, 1005), ("e4", 121, 999),
+                 ("e5", 120, 999), ("e6", 125, 750), ("e7", 120, 950), ("e8", 120, 700)]  # README.md:73-80
+README_LINES = ['{"0":["e1"],"1":["e2","e3","e4","e5"],"2":["e6"]}',  # README.md:93-96
+                '{"0":["e3"],"1":["e4"],"2":["e6"]}',
+                '{"0":["e1"],"1":["e2","e3","e4","e5","e6","e7"],"2":["e8"]}',
+                '{"0":["e3"],"1":["e4","e6"],"2":["e8"]}']
+T0 = 1_600_000_000_000
+
+
+def _java_hash(s: str) -> int:
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h
+
+
+def demo_json(seq: P.Sequence) -> str:
+    """The demo's `matches` processor (CEPStockKStreamsDemo.java:60-71): a JSONObject (a
+    HashMap of capacity 16: entries in bucket order) of stage -> names, oldest first."""
+    items = list(seq.as_map().items())
+    items.sort(key=lambda kv: ((_java_hash(kv[0]) ^ (_java_hash(kv[0]) >> 16)) & 15))
+    return "{" + ",".join(f'"{k}":' + json.dumps([e.value["name"] for e in reversed(v)], separators=(",", ":"))
+                          for k, v in items) + "}"
+
+
+def _factory(gpu):
+    return None if gpu else OracleStreamSession
+
+
+def run_records(pattern, records, batch_size, gpu, punctuate_every=0):
+    """Plays (key, value, timestamp) records into a processor; -> (context, processor)."""
+    ctx = P.RecordContext("StockEvents", 0)
+    proc = P.CEPProcessor(pattern, batch_size=batch_size, max_keys=1024, session_factory=_factory(gpu))
+    proc.init(ctx)
+    for i, (k, v, ts) in enumerate(records):
+        ctx.send(k, v, ts)
+        if punctuate_every and (i + 1) % punctuate_every == 0:
+            proc.punctuate(ts)
+    proc.close()
+    return ctx, proc
+
+
+def _readme_records(key="AAPL"):
+    return [(key, {"name": n, "price": p, "volume": v}, T0 + i) for i, (n, p, v) in enumerate(README_EVENTS)]
+
+
+def forwarded_view(ctx):
+    """Forwarded Sequences as [[(stage, [offsets in list order])...] in map order]."""
+    out = []
+    for k, seq in ctx.forwarded:
+        assert k is None  # context.forward(null, seq), CEPProcessor.java:161
+        out.append([(st, [e.offset for e in evs]) for st, evs in seq.as_map().items()])
+    return out
+
+
+def expected_view(pattern, records):
+    """One reference NFA per key over the whole stream (the oracle), matches in the order the
+    reference forwards them: by arrival of the completing record, emission order within it."""
+    ir = pattern.to_ir()
+    names = N.Query(ir).stage_names
+    keys = {}
+    kid = np.array([keys.setdefault(k, len(keys)) for k, _, _ in records], np.int64)
+    by_key = np.argsort(kid, kind="stable")
+    counts = np.bincount(kid, minlength=len(keys))
+    off = np.zeros(len(keys) + 1, np.uint64)
+    np.cumsum(counts, out=off[1:])
+    S = pattern.schema
+    cols = [np.array([r[1][n] for r in records], np.int32)[by_key] for n in S.names]
+    ts = np.array([r[2] for r in records], np.int64)[by_key]
+    r = oracle.run(ir, off, cols, ts)
+    emit = by_key[r["emit_pos"].astype(np.int64)]
+    out = []
+    for m in np.argsort(emit, kind="stable").tolist():
+        a, b = int(r["pair_off"][m]), int(r["pair_off"][m + 1])
+        seq = {}
+        for st, pos in zip(r["pair_stage"][a:b].tolist(), r["pair_pos"][a:b].tolist()):
+            seq.setdefault(names[st], []).append(int(by_key[pos]))
+        out.append(list(seq.items()))
+    err = [(int(by_key[int(r["err_pos"][j])]), int(r["err_code"][j])) for j in range(len(keys)) if r["err_code"][j]]
+    return out, emit, err
+
+
+def random_records(seed, n_keys=24, n=600):
+    rng = np.random.default_rng(seed)
+    price = {k: 100 + k % 7 for k in range(n_keys)}
+    recs = []
+    for i in range(n):
+        k = int(rng.integers(n_keys))
+        price[k] += int(rng.integers(-2, 3))
+        u = rng.random()
+        vol = int(rng.integers(1001, 1100)) if u < 0.15 else (int(rng.integers(300, 700)) if u < 0.35 else
+                                                             int(rng.integers(900, 1000)))
+        recs.append((f"k{k}", {"name": f"e{i}", "price": price[k], "volume": vol}, T0 + i))
+    return recs
+
+
+def arith_query():
+    """The README query with a trap in the first stage: `v.volume > 1000 && v.price / v.price
+    == 1` throws ArithmeticException on a begin candidate with price 0."""
+    S = W.stock_query("readme").schema
+    return (QueryBuilder(S).select()
+            .where(lambda k, v, ts, s: (v.volume > 1000) & (v.price / v.price == 1))
+            .fold("avg", lambda k, v, c: v.price).then()
+            .select().oneOrMore().skipTillNextMatch()
+            .where(lambda k, v, ts, s: v.price > s.get("avg"))
+            .fold("avg", lambda k, v, c: (c + v.price) / 2).fold("volume", lambda k, v, c: v.volume).then()
+            .select().skipTillNextMatch().where(lambda k, v, ts, s: v.volume < 0.8 * s.get("volume"))
+            .within(1, W.TimeUnit.HOURS).build())
+
+
+# ---- host logic (CPU) --------------------------------------------------------------------
+def test_event_and_sequence_semantics():
+    a = P.Event("k", 1, 10, "t", 0, 5)
+    assert a == P.Event("other", 2, 99, "t", 0, 5) and hash(a) == hash(P.Event(None, None, 0, "t", 0, 5))
+    assert a != P.Event("k", 1, 10, "t", 1, 5)
+    assert a.compare_to(P.Event("k", 1, 0, "t", 0, 6)) == -1  # same partition: offsets
+    assert a.compare_to(P.Event("k", 1, 0, "u", 0, 1)) == 1   # across partitions: timestamps
+    s1 = P.Sequence().add("0", a).add("1", P.Event("k", 1, 11, "t", 0, 6)).add("1", P.Event("k", 1, 12, "t", 0, 7))
+    s2 = P.Sequence().add("1", P.Event("k", 1, 12, "t", 0, 7)).add("1", P.Event("k", 1, 11, "t", 0, 6)).add("0", a)
+    assert s1 == s2 and s1.size() == 3 and [e.offset for e in s1.get("1")] == [6, 7]
+    assert s1 != P.Sequence().add("0", a)
+    assert P.Sequence().add("0", a) == s1  # one-directional, as Sequence.java:59-73
+
+
+@pytest.mark.parametrize("batch", [1, 3, 8, 1000])
+def test_readme_demo_cpu(batch):
+    ctx, _ = run_records(W.stock_query("readme"), _readme_records(), batch, gpu=False)
+    assert [demo_json(s) for _, s in ctx.forwarded] == README_LINES
+
+
+def test_null_values_skipped_cpu():
+    recs = _readme_records()
+    with_nulls = []
+    for r in recs:
+        with_nulls += [r, ("AAPL", None, r[2])]
+    ctx = P.RecordContext()
+    proc = P.CEPProcessor(W.stock_query("readme"), batch_size=2, session_factory=OracleStreamSession)
+    proc.init(ctx)
+    for k, v, ts in with_nulls:
+        ctx.send(k, v, ts)
+    proc.close()
+    assert [demo_json(s) for _, s in ctx.forwarded] == README_LINES
+
+
+@pytest.mark.parametrize("batch,punct", [(1, 0), (7, 0), (64, 5), (10_000, 0)])
+def test_interleaved_keys_forward_order_cpu(batch, punct):
+    recs = random_records(11, n_keys=12, n=300)
+    exp, _, err = expected_view(W.stock_query("readme"), recs)
+    assert not err and len(exp) > 5
+    ctx, _ = run_records(W.stock_query("readme"), recs, batch, gpu=False, punctuate_every=punct)
+    assert forwarded_view(ctx) == exp
+
+
+def _arith_records():
+    recs = random_records(5, n_keys=6, n=200)
+    bad = 120
+    k = recs[bad][0]
+    recs[bad] = (k, {"name": "bad", "price": 0, "volume": 1500}, recs[bad][2])
+    return recs, bad
+
+
+def _check_error_run(gpu, batch):
+    q = arith_query()
+    recs, bad = _arith_records()
+    exp, emit, err = expected_view(q, recs)
+    assert err == [(bad, 3)]
+    n_before = int(np.sum(emit < bad))
+    assert 0 < n_before < len(exp)  # matches both before and after the failing record
+    ctx = P.RecordContext("StockEvents", 0)
+    proc = P.CEPProcessor(q, batch_size=batch, max_keys=64, session_factory=_factory(gpu))
+    proc.init(ctx)
+    with pytest.raises(P.ArithmeticException) as ei:
+        for k, v, ts in recs:
+            ctx.send(k, v, ts)
+        proc.close()
+    assert ei.value.event.offset == bad and ei.value.key == recs[bad][0]
+    assert forwarded_view(ctx) == exp[:n_before]
+    with pytest.raises(P.ArithmeticException):
+        proc.process("k0", {"name": "x", "price": 1, "volume": 1})
+    proc.close()
+
+
+@pytest.mark.parametrize("batch", [1, 16, 1000])
+def test_key_exception_after_earlier_matches_cpu(batch):
+    _check_error_run(False, batch)
+
+
+# ---- through libcep on the GPU -----------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 3, 1000])
+def test_readme_demo_gpu(batch):
+    ctx, _ = run_records(W.stock_query("readme"), _readme_records(), batch, gpu=True)
+    assert [demo_json(s) for _, s in ctx.forwarded] == README_LINES
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,punct", [(5, 0), (97, 0), (4096, 250)])
+def test_interleaved_keys_forward_order_gpu(batch, punct):
+    recs = random_records(11, n_keys=200, n=3000)
+    exp, _, err = expected_view(W.stock_query("readme"), recs)
+    assert not err and len(exp) > 20
+    ctx, _ = run_records(W.stock_query("readme"), recs, batch, gpu=True, punctuate_every=punct)
+    assert forwarded_view(ctx) == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 16, 1000])
+def test_key_exception_after_earlier_matches_gpu(batch):
+    _check_error_run(True, batch)
