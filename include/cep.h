@@ -238,6 +238,13 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size);
 
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);
 
+/* The same device times summed over every batch since the last reset (reset != 0 zeroes
+ * them after reading), and the number of batches.  Stencil batches return from
+ * cep_push_batch without a host sync (pushes queue on the session stream); their event
+ * pairs are read here and by every result call (poll, digest, timing, watermark), so a
+ * caller can push many batches and time them all without stalling the pipeline. */
+int cep_timing_totals(cep_session* s, int query, int reset, double* kernel_ms, double* aux_ms, uint64_t* batches);
+
 /* Where the last batch's NFA work went, for query `query`'s kernel group (queries sharing a
  * launch report the same group figures; stencil queries report zeros but kernel_ms). */
 typedef struct {

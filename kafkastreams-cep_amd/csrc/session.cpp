@@ -76,6 +76,16 @@ template <class T> struct HVec {  // host copy of a result array
   std::vector<T> v;
 };
 
+struct Scratch {  // small counters, one allocation
+  uint32_t node_top, pred_top, out_top, n_cap_err;
+  uint32_t tile_counter, overflow, n_retry_cap, n_retry_conflict;
+  uint32_t job_next, pad2;
+  uint64_t totals[2];
+  uint64_t total;
+  unsigned long long digest;
+  unsigned long long wmax;
+};
+
 // A streaming session's per-query NFA state (cep_opts.streaming): every key's run queue,
 // buffer pools and carried lane state persist from one batch to the next.
 struct StreamState {
@@ -111,6 +121,25 @@ struct QueryRt {
   float aux_ms = 0;     // setup and compaction kernels of the same batch
   uint32_t launches = 0;
   StreamState st;
+  // Stencil batches return without a host sync (pushes pipeline on the stream): the match
+  // count comes back through pinned memory and each batch's event triple (setup start,
+  // kernels start, end) goes into a ring, all read when a result is asked for (resolve()).
+  static constexpr int kRing = 16;
+  Scratch* h_sc = nullptr;  // pinned copy of the batch's counters
+  bool pending = false;
+  hipEvent_t tev[kRing][3] = {};
+  bool tev_used[kRing] = {};
+  int tev_next = 0, tev_last = -1;
+  uint64_t ks_zeroed = 0;  // stencil: KeyState entries known zero
+  // every batch's timing since the last cep_timing_totals reset
+  double acc_kernel_ms = 0, acc_aux_ms = 0;
+  uint64_t acc_batches = 0;
+  ~QueryRt() {
+    for (auto& t : tev)
+      for (auto& e : t)
+        if (e) (void)hipEventDestroy(e);
+    if (h_sc) (void)hipHostFree(h_sc);
+  }
 };
 
 // Queries whose NFA kernels run as one launch (compile.cpp plan_groups): lanes are (query,
@@ -156,6 +185,8 @@ struct cep_session {
   const int64_t* ts = nullptr;
   Cols cols{};
   int64_t watermark = INT64_MIN;
+  unsigned long long* h_wm = nullptr;  // pinned: the batch's max timestamp (read by resolve())
+  bool wm_pending = false;
   // arrival-order batches: device copies of the input, the partitioned (CSR) batch
   DBuf a_keys, a_ts, p_off, p_cnt, p_ts, p_perm, p_sorted, p_idx, p_scratch;
   DBuf a_cols[kMaxFields], p_cols[kMaxFields];
@@ -180,44 +211,78 @@ struct DeviceGuard {
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
-struct Scratch {  // small counters, one allocation
-  uint32_t node_top, pred_top, out_top, n_cap_err;
-  uint32_t tile_counter, overflow, n_retry_cap, n_retry_conflict;
-  uint32_t job_next, pad2;
-  uint64_t totals[2];
-  uint64_t total;
-  unsigned long long digest;
-  unsigned long long wmax;
-};
+// a ring slot's timing into the query's totals (its events are waited for)
+void ring_take(QueryRt& r, int i) {
+  HIPCHECK(hipEventSynchronize(r.tev[i][2]));
+  float a = 0, k = 0;
+  HIPCHECK(hipEventElapsedTime(&a, r.tev[i][0], r.tev[i][1]));
+  HIPCHECK(hipEventElapsedTime(&k, r.tev[i][1], r.tev[i][2]));
+  r.acc_kernel_ms += k;
+  r.acc_aux_ms += a;
+  r.acc_batches++;
+  r.tev_used[i] = false;
+  if (i == r.tev_last) {
+    r.kernel_ms = k;
+    r.aux_ms = a;
+  }
+}
 
+// The host side of the last batch's asynchronous results (stencil counts and timing, the
+// watermark): one stream sync, then the pinned copies are read.
+void resolve(cep_session* s) {
+  bool any = s->wm_pending;
+  for (auto& r : s->qs) any = any || r->pending;
+  if (!any) return;
+  HIPCHECK(hipStreamSynchronize(s->stream));
+  for (auto& rp : s->qs) {
+    QueryRt& r = *rp;
+    if (!r.pending) continue;
+    for (int i = 0; i < QueryRt::kRing; i++)
+      if (r.tev_used[i]) ring_take(r, i);
+    r.pending = false;
+    if (r.h_sc->overflow) throw std::runtime_error("stencil output overflow");
+    r.n_matches = r.h_sc->total;
+    r.n_pairs = r.n_matches * r.arity;
+  }
+  if (s->wm_pending) {
+    s->watermark = (int64_t)(*s->h_wm ^ 0x8000000000000000ull);
+    s->wm_pending = false;
+  }
+}
+
+// Strict chains (stencil.hip): wave_keys, stencil_mask, stencil_emit; no host sync.
 void run_stencil(cep_session* s, QueryRt& r) {
   const cep_query* q = r.q;
   const uint32_t m = q->info.arity;
   const uint64_t nk = s->n_keys;
   const uint64_t n_tiles = stencil_tiles(s->n_events);
-  const uint64_t nb = (nk + 1023) / 1024;
-  s->tile_key.ensure(sizeof(uint32_t) * 2 * (n_tiles + 1));                    // tile rank + count
-  s->status.ensure(sizeof(uint32_t) * (n_tiles / 64 + 2));                       // group counts
+  const uint64_t n_groups = n_tiles / 64 + 2;
+  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));                          // tile counts
+  s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
   s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
-  s->keylist.ensure(sizeof(uint32_t) * (2 * nk + nb + 2));                       // rank, nz_key, bsum
-  s->bnd.ensure(sizeof(uint64_t) * (s->n_events / 64 + 8));
-  s->scratch.ensure(sizeof(Scratch));
+  s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
+  s->bnd.ensure(sizeof(uint32_t) * (s->n_events / 64 + 2));                       // word -> key
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
   r.m_key.ensure(sizeof(uint32_t) * cap);
   r.p_seq.ensure(sizeof(uint32_t) * cap * m);
-  Scratch* sc = s->scratch.as<Scratch>();
-  uint32_t* rank = s->keylist.as<uint32_t>();
-  uint32_t* nz_key = rank + nk;
-  uint32_t* bsum = nz_key + nk;
-  HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
+  if (!r.h_sc) HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocDefault));
+  if (!r.tev[0][0])
+    for (auto& t : r.tev)
+      for (auto& e : t) HIPCHECK(hipEventCreate(&e));
+  const int slot = r.tev_next;
+  if (r.tev_used[slot]) ring_take(r, slot);  // kRing batches back: long done
+  r.tev_next = (slot + 1) % QueryRt::kRing;
+  r.tev_last = slot;
+  r.tev_used[slot] = true;
+
+  Scratch* sc = s->status.as<Scratch>();
   StencilArgs a{};
   a.n_keys = nk;
   a.n_events = s->n_events;
   a.key_off = s->key_off;
-  a.bnd = s->bnd.as<uint64_t>();
-  a.tile_rank = s->tile_key.as<uint32_t>();
-  a.nz_key = nz_key;
+  a.wave_key = s->keylist.as<uint32_t>();
+  a.word_key = s->bnd.as<uint32_t>();
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.cols = s->cols;
@@ -234,37 +299,31 @@ void run_stencil(cep_session* s, QueryRt& r) {
   }
   for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
-  a.tile_cnt = s->tile_key.as<uint32_t>() + (n_tiles + 1);
-  a.group_cnt = s->status.as<uint32_t>();
+  a.tile_cnt = s->tile_key.as<uint32_t>();
+  a.group_cnt = reinterpret_cast<uint32_t*>(sc + 1);
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
   a.total = &sc->total;
   a.out_cap = cap;
   a.overflow = &sc->overflow;
-  HIPCHECK(hipEventRecord(s->ev2, s->stream));
-  HIPCHECK(hipMemsetAsync(s->bnd.p, 0, sizeof(uint64_t) * (s->n_events / 64 + 8), s->stream));
-  HIPCHECK(hipMemsetAsync(s->status.p, 0, sizeof(uint32_t) * (n_tiles / 64 + 2), s->stream));
-  HIPCHECK(launch_key_index(s->key_off, nk, s->n_events, rank, bsum, nz_key, s->bnd.as<uint64_t>(),
-                            s->tile_key.as<uint32_t>(), s->stream));
-  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  HIPCHECK(hipEventRecord(r.tev[slot][0], s->stream));
+  HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch) + sizeof(uint32_t) * n_groups, s->stream));
+  HIPCHECK(launch_wave_keys(s->key_off, nk, s->n_events, s->keylist.as<uint32_t>(), s->stream));
+  HIPCHECK(hipEventRecord(r.tev[slot][1], s->stream));
   HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->stream));
-  HIPCHECK(hipEventRecord(s->ev1, s->stream));
-  Scratch h{};
-  HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
-  HIPCHECK(hipStreamSynchronize(s->stream));
-  HIPCHECK(hipEventElapsedTime(&r.kernel_ms, s->ev0, s->ev1));
-  HIPCHECK(hipEventElapsedTime(&r.aux_ms, s->ev2, s->ev0));
+  HIPCHECK(hipEventRecord(r.tev[slot][2], s->stream));
+  HIPCHECK(hipMemcpyAsync(r.h_sc, sc, sizeof(Scratch), hipMemcpyDeviceToHost, s->stream));
+  r.pending = true;
   r.launches = 2;  // stencil_mask + stencil_emit
-  if (h.overflow) throw std::runtime_error("stencil output overflow");
-  r.n_matches = h.total;
-  r.n_pairs = h.total * m;
   r.digest_valid = false;
   r.arity = m;
   // no per-key errors on this path: the predicates and folds are total
-  r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
-  HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * nk, s->stream));
+  if (r.ks_zeroed < nk) {
+    r.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(nk, 1));
+    HIPCHECK(hipMemsetAsync(r.ks.p, 0, sizeof(KeyState) * nk, s->stream));
+    r.ks_zeroed = nk;
+  }
   r.ks_dev = r.ks.as<KeyState>();
-  HIPCHECK(hipStreamSynchronize(s->stream));
 }
 
 hipError_t launch_nfa_tier(GroupRt& g, const cep_query* q0, NfaArgs& a, uint64_t nslots, hipStream_t st) {
@@ -498,8 +557,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
     while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
     a.rcap = rcap;
     s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
-    s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));
+    s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));  // (may move: re-read below)
     a.rings = s->retry_rings.p;
+    a.walks = s->walks.p;
     a.order = nullptr;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
     for (int k = 0; k < 2; k++) {  // capacity re-runs keep deferred walks, conflicts walk in place
@@ -563,6 +623,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
     r.arity = 0;
     r.kernel_ms = total_ms;  // the group's matching launches
     r.launches = launches;
+    r.acc_kernel_ms += r.kernel_ms;
+    r.acc_aux_ms += r.aux_ms;
+    r.acc_batches++;
   }
 }
 
@@ -762,6 +825,7 @@ void cep_session_destroy(cep_session* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     s->groups.clear();
     s->qs.clear();
+    if (s->h_wm) (void)hipHostFree(s->h_wm);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->ev2) (void)hipEventDestroy(s->ev2);
@@ -845,6 +909,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     for (auto& r : s->qs) {
       r->have = false;
       r->host_valid = false;
+      r->pending = false;  // (its timing stays in the ring: still accumulated)
     }
     s->arrival = b->arrival_key != nullptr;
     s->partition_ms = 0;
@@ -877,15 +942,15 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     }
     // watermark
     s->watermark = INT64_MIN;
-    if (s->ts && s->n_events) {
+    s->wm_pending = false;
+    if (s->ts && s->n_events) {  // read back with the batch's other results (resolve())
       s->scratch.ensure(sizeof(Scratch));
       Scratch* sc = s->scratch.as<Scratch>();
+      if (!s->h_wm) HIPCHECK(hipHostMalloc((void**)&s->h_wm, sizeof(unsigned long long), hipHostMallocDefault));
       HIPCHECK(hipMemsetAsync(&sc->wmax, 0, sizeof(unsigned long long), s->stream));
       HIPCHECK(launch_max(s->ts, s->n_events, &sc->wmax, s->stream));
-      unsigned long long w = 0;
-      HIPCHECK(hipMemcpyAsync(&w, &sc->wmax, sizeof w, hipMemcpyDeviceToHost, s->stream));
-      HIPCHECK(hipStreamSynchronize(s->stream));
-      s->watermark = (int64_t)(w ^ 0x8000000000000000ull);
+      HIPCHECK(hipMemcpyAsync(s->h_wm, &sc->wmax, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+      s->wm_pending = true;
     }
     if (s->groups.size() && (uint64_t)s->qs.size() * s->n_keys >= 0xFFFFFFFFull)
       throw std::invalid_argument("queries x keys of a batch must stay below 2^32 (job ids are u32)");
@@ -936,6 +1001,7 @@ int cep_poll_matches(cep_session* s, int query, int memory, cep_matches* out) {
   if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
   return guarded([&] {
     DeviceGuard g(s->device);
+    resolve(s);
     std::memset(out, 0, sizeof *out);
     out->n_matches = r.n_matches;
     out->n_pairs = r.n_pairs;
@@ -1003,6 +1069,8 @@ int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* c
   QueryRt& r = *s->qs[query];
   if (!r.have) return fail(CEP_E_STATE, "no batch has been pushed");
   return guarded([&] {
+    DeviceGuard g0(s->device);
+    resolve(s);
     if (checksum && !r.digest_valid) {
       DeviceGuard g(s->device);
       s->scratch.ensure(sizeof(Scratch));
@@ -1022,8 +1090,11 @@ int cep_match_digest(cep_session* s, int query, uint64_t* n_matches, uint64_t* c
 
 int cep_watermark(cep_session* s, int64_t* out) {
   if (!s || !out) return fail(CEP_E_INVALID, "null argument");
-  *out = s->watermark;
-  return CEP_OK;
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    resolve(s);
+    *out = s->watermark;
+  });
 }
 
 // ---- streaming-session snapshot / restore ----
@@ -1181,25 +1252,49 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size) {
 
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches) {
   if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
-  if (kernel_ms) *kernel_ms = s->qs[query]->kernel_ms;
-  if (aux_ms) *aux_ms = s->qs[query]->aux_ms;
-  if (launches) *launches = s->qs[query]->launches;
-  return CEP_OK;
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    resolve(s);
+    if (kernel_ms) *kernel_ms = s->qs[query]->kernel_ms;
+    if (aux_ms) *aux_ms = s->qs[query]->aux_ms;
+    if (launches) *launches = s->qs[query]->launches;
+  });
+}
+
+int cep_timing_totals(cep_session* s, int query, int reset, double* kernel_ms, double* aux_ms, uint64_t* batches) {
+  if (!s || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    resolve(s);
+    QueryRt& r = *s->qs[query];
+    for (int i = 0; i < QueryRt::kRing; i++)
+      if (r.tev_used[i]) ring_take(r, i);
+    if (kernel_ms) *kernel_ms = r.acc_kernel_ms;
+    if (aux_ms) *aux_ms = r.acc_aux_ms;
+    if (batches) *batches = r.acc_batches;
+    if (reset) {
+      r.acc_kernel_ms = r.acc_aux_ms = 0;
+      r.acc_batches = 0;
+    }
+  });
 }
 
 int cep_last_stats(cep_session* s, int query, cep_batch_stats* out) {
   if (!s || !out || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
-  const QueryRt& r = *s->qs[query];
-  if (r.group < 0) {
-    *out = cep_batch_stats{};
-    out->group = 0xFFFFFFFFu;
-    out->kernel_ms = out->main_ms = r.kernel_ms;
-    out->launches = r.launches;
-    return CEP_OK;
-  }
-  *out = s->groups[r.group]->stats;
-  out->group = (uint32_t)r.group;
-  return CEP_OK;
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    resolve(s);
+    const QueryRt& r = *s->qs[query];
+    if (r.group < 0) {
+      *out = cep_batch_stats{};
+      out->group = 0xFFFFFFFFu;
+      out->kernel_ms = out->main_ms = r.kernel_ms;
+      out->launches = r.launches;
+      return;
+    }
+    *out = s->groups[r.group]->stats;
+    out->group = (uint32_t)r.group;
+  });
 }
 
 int cep_gather_keys(int device, uint64_t n_sel, const uint32_t* sel_keys, const uint64_t* src_key_off,

@@ -39,62 +39,39 @@ constexpr uint64_t kStTile = (uint64_t)kStThreads * kStPer;
 constexpr uint64_t kStGroup = 64;  // tiles per group count (stencil_emit's offsets)
 
 // ---------------------------------------------------------------- per-batch key index
-// rank[k] = number of non-empty keys before k (two-level exclusive scan)
-__global__ void __launch_bounds__(1024) nz_rank_blocks(const uint64_t* key_off, uint64_t n_keys, uint32_t* rank,
-                                                       uint32_t* bsum) {
-  __shared__ uint32_t s[1024];
-  const uint64_t k = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-  const uint32_t f = (k < n_keys && key_off[k + 1] > key_off[k]) ? 1u : 0u;
-  s[threadIdx.x] = f;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t y = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += y;
-    __syncthreads();
-  }
-  if (k < n_keys) rank[k] = s[threadIdx.x] - f;
-  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
-}
+constexpr int kStWave = kStTile / (kStThreads / 64);  // 4096 events per wave of stencil_mask
+constexpr int kWkInline = 16;  // wave starts a thread writes itself; longer keys: the block
 
-__global__ void __launch_bounds__(1024) nz_rank_top(uint32_t* bsum, uint64_t nb) {
-  __shared__ uint32_t t[1024];
-  const uint64_t per = (nb + 1023) / 1024;
-  const uint64_t a = threadIdx.x * per, b = (a + per < nb) ? a + per : nb;
-  uint32_t sum = 0;
-  for (uint64_t i = a; i < b; i++) sum += bsum[i];
-  t[threadIdx.x] = sum;
+// wave_key[w] = the key holding event w * kStWave (wave starts inside key k: ceil(s/W) ..
+// ceil(e/W) - 1; empty keys hold none).  A thread per key; a key spanning more than kWkInline
+// wave starts is written by its whole block (a single key of the whole stream stays parallel).
+__global__ void __launch_bounds__(256) wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_waves,
+                                                 uint32_t* wave_key) {
+  __shared__ uint32_t s_big[256];
+  __shared__ uint32_t s_nbig;
+  if (threadIdx.x == 0) s_nbig = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < 1024; i++) {
-      const uint32_t x = t[i];
-      t[i] = acc;
-      acc += x;
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n_keys) {
+    const uint64_t s = key_off[k], e = key_off[k + 1];
+    const uint64_t w0 = (s + kStWave - 1) / kStWave;
+    uint64_t w1 = (e + kStWave - 1) / kStWave;
+    w1 = w1 < n_waves ? w1 : n_waves;
+    if (w1 > w0 + kWkInline) {
+      s_big[atomicAdd(&s_nbig, 1u)] = (uint32_t)k;
+    } else {
+      for (uint64_t w = w0; w < w1; w++) wave_key[w] = (uint32_t)k;
     }
   }
   __syncthreads();
-  uint32_t o = t[threadIdx.x];
-  for (uint64_t i = a; i < b; i++) {
-    const uint32_t x = bsum[i];
-    bsum[i] = o;
-    o += x;
+  const uint32_t nbig = s_nbig;
+  for (uint32_t i = 0; i < nbig; i++) {
+    const uint32_t kk = s_big[i];
+    const uint64_t w0 = (key_off[kk] + kStWave - 1) / kStWave;
+    uint64_t w1 = (key_off[kk + 1] + kStWave - 1) / kStWave;
+    w1 = w1 < n_waves ? w1 : n_waves;
+    for (uint64_t w = w0 + threadIdx.x; w < w1; w += 256) wave_key[w] = kk;
   }
-}
-
-// non-empty key k: nz_key[rank] = k, its start bit, and the rank of every tile whose first
-// event lies inside it
-__global__ void __launch_bounds__(256) key_index(const uint64_t* key_off, uint64_t n_keys, const uint32_t* rank,
-                                                 const uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd,
-                                                 uint32_t* tile_rank, uint64_t n_tiles) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n_keys) return;
-  const uint64_t s = key_off[k], e = key_off[k + 1];
-  if (s == e) return;
-  const uint32_t r = rank[k] + bsum[k / 1024];
-  nz_key[r] = (uint32_t)k;
-  atomicOr((unsigned long long*)&bnd[s / 64], 1ull << (s % 64));
-  for (uint64_t t = (s + kStTile - 1) / kStTile; t * kStTile < e && t < n_tiles; t++) tile_rank[t] = r;
 }
 
 // ---------------------------------------------------------------- the stencil
@@ -112,7 +89,6 @@ __device__ __forceinline__ bool in_range(int64_t v, int64_t lo, int64_t hi) { re
 // into 4-bit nibbles; the window needs the M-1 <= 7 events before the nibble, i.e. the
 // nibbles of lanes l-1 and l-2 (cross-lane shuffles) or, for lanes 0-1, of lanes 62-63 of
 // the previous step (wave-uniform carries).  Key starts come the same way from the bitmap.
-constexpr int kStWave = kStTile / (kStThreads / 64);  // 4096 events per wave
 constexpr int kStSteps = kStWave / 256;               // 16 load steps per wave
 constexpr int kStDefaultPF = 1;
 
@@ -217,12 +193,10 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
       yb[d] = NCOL > 1 ? __builtin_nontemporal_load(c1 + d * 64) : xb[d];
     }
   }
-  // the wave's 64 key-start words, one per lane (word w: events 64 w .. 64 w + 63)
-  // (all of the wave's start-up loads are unconditional, clamped in bounds and issued
-  // together: one memory round trip before the first step, not three)
-  const uint64_t last_word = (A.n_events - 1) / 64;  // n_events >= 1: the tile exists
-  const uint64_t bwi = wbase / 64 + lane;
-  const uint64_t bwl = H > 0 ? A.bnd[bwi < last_word ? bwi : last_word] : 0;
+  // the key holding the wave's first event (wave_keys); the seed loads below go out with it
+  const uint64_t n_waves = (A.n_events + kStWave - 1) / kStWave;  // n_events >= 1: the tile exists
+  const uint64_t wi = wbase / kStWave;
+  const uint32_t k0 = A.wave_key[wi < n_waves ? wi : n_waves - 1];
   // the 8 events before the wave (lanes 0..7; the others load the same lines)
   const uint64_t sp0 = (wbase >= 8 ? wbase - 8 : 0) + (uint64_t)(lane & 7);
   const uint64_t sp = sp0 < A.n_events ? sp0 : A.n_events - 1;
@@ -231,10 +205,41 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
     sx0 = A.col[0][sp];
     sx1 = A.col[NCOL - 1][sp];
   }
-  // the key-start word before the wave (wbase % 64 == 0)
-  const uint64_t bprev = H > 0 ? A.bnd[wbase >= 64 ? wbase / 64 - 1 : 0] : 0;
   if (RANGE && H > 0) asm volatile("" ::"v"(sx0), "v"(sx1));  // keeps the seed loads up here
-  const uint64_t bw = (wbase + (uint64_t)lane * 64 < A.n_events) ? bwl : 0;
+  // Key starts in [wbase - 8, wend): lanes read key_off[k0 - 8 + 64 c + lane] (the 8 keys
+  // before k0 may start among the 8 events before the wave) and a wave-uniform loop visits
+  // the starts in range, in key order.  bw: this lane's start bits (events wbase + 64 lane
+  // ..+63), pkb: starts among the 8 events before the wave (bit x: event wbase - 8 + x),
+  // wkey: the key holding event wbase + 64 lane (for stencil_emit: the largest key whose
+  // offset is <= it; empty keys share their successor's offset and lose to it).
+  const uint64_t wend = wbase + kStWave < A.n_events ? wbase + kStWave : A.n_events;
+  const uint64_t lo = wbase >= 8 ? wbase - 8 : 0;
+  const uint64_t ws = wbase + (uint64_t)lane * 64;
+  uint64_t bw = 0;
+  uint32_t pkb = 0, wkey = k0;
+  if (wbase < A.n_events) {
+    for (int64_t i0 = (int64_t)k0 - 8;; i0 += 64) {
+      const int64_t i = i0 + lane;
+      const bool valid = i >= 0 && (uint64_t)i < A.n_keys;
+      const uint64_t sj = valid ? A.key_off[i] : 0;
+      uint64_t inr = __ballot(valid && sj >= lo && sj < wend);
+      while (inr) {
+        const int j = __builtin_ctzll(inr);
+        inr &= inr - 1;
+        const uint64_t sjj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sj >> 32), j) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, j);
+        if (sjj >= wbase) {
+          if (((sjj - wbase) >> 6) == (uint64_t)lane) bw |= 1ull << (sjj & 63);
+        } else {
+          pkb |= 1u << (uint32_t)(sjj - (wbase - 8));
+        }
+        if (sjj <= ws) wkey = (uint32_t)(i0 + j);
+      }
+      const uint64_t s63 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sj >> 32), 63) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, 63);
+      if (!(i0 + 64 < (int64_t)A.n_keys && s63 < wend)) break;  // no key after this chunk starts in range
+    }
+  }
   // steps with a key start (bit 4q + x: word x of step q is non-zero), mostly none
   const uint64_t kstep = H > 0 ? __ballot(bw != 0) : 0;
   // Ballot words of the previous step: bit l of W[s][k] = stage s holds at event 4l + k.
@@ -255,9 +260,9 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
 #pragma unroll
       for (int k = 0; k < 4; k++) pW[s][k] = (((b >> k) & 1ull) << 62) | (((b >> (4 + k)) & 1ull) << 63);
     }
-    const uint64_t w = (H > 0 && wbase >= 8) ? bprev : 0;
+    const uint32_t pb = (H > 0 && wbase >= 8) ? pkb : 0u;
 #pragma unroll
-    for (int k = 0; k < 4; k++) pK[k] = (((w >> (56 + k)) & 1ull) << 62) | (((w >> (60 + k)) & 1ull) << 63);
+    for (int k = 0; k < 4; k++) pK[k] = (((uint64_t)(pb >> k) & 1ull) << 62) | (((uint64_t)(pb >> (4 + k)) & 1ull) << 63);
   }
   bool pk_any = ((pK[0] | pK[1] | pK[2] | pK[3]) >> 62) != 0;
   uint64_t myword = 0;  // mask word wbase / 64 + lane = word k of step q for lane 4q + k
@@ -374,6 +379,7 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   }
   // one 512-B store: words 4q..4q+3 belong to step q (written when the step has an event)
   if (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) A.mask[wbase / 64 + lane] = myword;
+  if (ws < A.n_events) A.word_key[wbase / 64 + lane] = wkey;
   // matches of the wave: popcount of each lane's word, summed over the wave once
   uint32_t cnt = (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) ? (uint32_t)__popcll(myword) : 0u;
 #pragma unroll
@@ -398,7 +404,8 @@ __device__ __forceinline__ uint64_t spread4(uint32_t x16) {
 }
 
 // Pass 2: a thread per 64 events (a quarter of a step's ballot words), the tile's offset
-// from the group and tile counts, a block scan for the threads' offsets and key ranks.
+// from the group and tile counts, a block scan for the threads' offsets.  A match's key is
+// the thread's first key (word_key) advanced over the key offsets it passes.
 template <int M>
 __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   // a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
@@ -411,32 +418,28 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
   // Every independent load is issued before the first use (addresses clamped, no branches):
   // the step (256 events) holding this thread's 64 - 16 lanes of each of its 4 ballot words -
-  // its key-start word, the tile's first key (rank -> key -> CSR start, scalar loads) and
-  // the counts of the tiles before it.
+  // its first key, and the counts of the tiles before it.
   const bool valid = p0 < A.n_events;
   const uint64_t pc = valid ? p0 : t * kStTile;  // a tile's first event always exists
   const uint64_t* w = A.mask + (pc / 256) * 4;
   const uint64_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-  const uint64_t Bw = A.bnd[pc / 64];
-  const uint32_t trank = A.tile_rank[t];
-  const uint32_t tkey = A.nz_key[trank];
-  const uint64_t tkstart = A.key_off[tkey];
+  uint32_t key = A.word_key[pc / 64];
   uint32_t ck[4] = {0, 0, 0, 0};
-  uint64_t B = 0;
   if (valid) {
     const int sh = 16 * (int)((p0 / 64) & 3);
     ck[0] = (uint32_t)(w0 >> sh) & 0xFFFFu;
     ck[1] = (uint32_t)(w1 >> sh) & 0xFFFFu;
     ck[2] = (uint32_t)(w2 >> sh) & 0xFFFFu;
     ck[3] = (uint32_t)(w3 >> sh) & 0xFFFFu;
-    B = Bw;
   }
-  const uint64_t Bk = (tid == 0) ? (B & ~1ull) : B;  // key starts after the tile's first event
   const uint32_t cnt = __popc(ck[0]) + __popc(ck[1]) + __popc(ck[2]) + __popc(ck[3]);
-  const uint32_t bc = (uint32_t)__popcll(Bk);
-  // block exclusive scan of (matches, key starts), packed 16|16 (each <= 16384 per tile)
-  const uint32_t packed = (cnt << 16) | bc;
-  uint32_t incl = packed;
+  uint64_t kstart = 0, knext = 0;
+  if (cnt) {
+    kstart = A.key_off[key];
+    knext = A.key_off[key + 1];
+  }
+  // block exclusive scan of the match counts
+  uint32_t incl = cnt;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(incl, o, 64);
@@ -457,27 +460,23 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
 #pragma unroll
   for (int w = 0; w < kStThreads / 64; w++)
     if (w < wv) woff += s_wsum[w];
-  const uint32_t excl = woff + incl - packed;
+  const uint32_t excl = woff + incl - cnt;
   const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
-  if (t + 1 == gridDim.x && tid == kStThreads - 1) *A.total = toff + ((woff + incl) >> 16);  // all matches
-  const uint32_t tile_total = (s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3]) >> 16;
+  if (t + 1 == gridDim.x && tid == kStThreads - 1) *A.total = toff + woff + incl;  // all matches
+  const uint32_t tile_total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
   const bool staged = tile_total <= kStage;  // block-uniform
-  uint64_t o = toff + (excl >> 16);
-  uint32_t so = excl >> 16;  // slot within the tile
-  const uint32_t rank0 = trank + (excl & 0xFFFF);
-  uint32_t cur_rank = trank, key = tkey;
-  uint64_t kstart = tkstart;
+  uint64_t o = toff + excl;
+  uint32_t so = excl;  // slot within the tile
   // natural order: event p0 + 4 l + k is bit l of ck[k] -> bit 4 l + k
   uint64_t match = spread4(ck[0]) | (spread4(ck[1]) << 1) | (spread4(ck[2]) << 2) | (spread4(ck[3]) << 3);
   while (match) {
     const int i = __builtin_ctzll(match);
     match &= match - 1;
     const uint64_t p = p0 + i;
-    const uint32_t rk = rank0 + (uint32_t)__popcll(Bk & (i == 63 ? ~0ull : ((2ull << i) - 1)));
-    if (rk != cur_rank) {
-      cur_rank = rk;
-      key = A.nz_key[rk];
-      kstart = A.key_off[key];
+    while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
+      key++;
+      kstart = knext;
+      knext = A.key_off[key + 1];
     }
     const uint32_t seq = (uint32_t)(p - kstart);
     if (staged) {
@@ -512,18 +511,16 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
 }
 
 // ---------------------------------------------------------------- host launchers
-hipError_t launch_key_index(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* rank,
-                            uint32_t* bsum, uint32_t* nz_key, uint64_t* bnd, uint32_t* tile_rank,
+hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
                             hipStream_t st) {
-  const uint64_t n_tiles = (n_events + kStTile - 1) / kStTile;
-  if (n_keys == 0 || n_tiles == 0) return hipSuccess;
-  const uint64_t nb = (n_keys + 1023) / 1024;
-  hipLaunchKernelGGL(nz_rank_blocks, dim3((uint32_t)nb), dim3(1024), 0, st, key_off, n_keys, rank, bsum);
-  hipLaunchKernelGGL(nz_rank_top, dim3(1), dim3(1024), 0, st, bsum, nb);
-  hipLaunchKernelGGL(key_index, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, rank, bsum,
-                     nz_key, bnd, tile_rank, n_tiles);
+  const uint64_t n_waves = (n_events + kStWave - 1) / kStWave;
+  if (n_keys == 0 || n_waves == 0) return hipSuccess;
+  hipLaunchKernelGGL(wave_keys, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, n_waves,
+                     wave_key);
   return hipGetLastError();
 }
+
+uint64_t stencil_waves(uint64_t n_events) { return (n_events + kStWave - 1) / kStWave; }
 
 // prefetch depth of stencil_mask's fast path (steps of 256 events whose loads run ahead);
 // CEP_STENCIL_PF (1, 2 or 4) overrides it for measurement

@@ -12,9 +12,7 @@ struct RangeStage {  // conjunction of lo <= col_c <= hi for c in {0, 1}
 struct StencilArgs {
   uint64_t n_keys, n_events;
   const uint64_t* key_off;
-  const uint64_t* bnd;       // bit p: a non-empty key starts at event p
-  const uint32_t* tile_rank; // rank (among non-empty keys) of the key holding each tile's first event
-  const uint32_t* nz_key;    // rank -> key id
+  const uint32_t* wave_key;  // key holding the first event of each wave's span (kStWave events)
   const int32_t* col[2];     // range fast path: up to two int columns
   RangeStage rs[8];
   // generic path (interpreted predicates)
@@ -27,6 +25,7 @@ struct StencilArgs {
   bool aligned;              // col[] 16-B aligned: vector loads
   // pass 1 -> pass 3
   uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k
+  uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1)
   uint32_t* tile_cnt;        // matches per tile (pass 1)
   uint32_t* group_cnt;       // matches per 64 tiles (pass 1, atomics; zeroed per batch)
   // output

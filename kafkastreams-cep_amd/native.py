@@ -27,7 +27,7 @@ EXPORTS = [
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
     "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
-    "cep_last_stats", "cep_gather_keys", "cep_synth_ts",
+    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals",
 ]
 
 
@@ -94,6 +94,8 @@ def lib():
             "cep_watermark": ([vp, C.POINTER(C.c_int64)], C.c_int),
             "cep_last_timing": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u32)],
                                 C.c_int),
+            "cep_timing_totals": ([vp, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(u64)],
+                                  C.c_int),
             "cep_last_error": ([], C.c_char_p),
             "cep_last_stats": ([vp, C.c_int, C.POINTER(BatchStats)], C.c_int),
             "cep_synth_ts": ([C.c_int, u64, C.c_int64, vp], C.c_int),
@@ -493,6 +495,12 @@ class Session:
         """(matching-kernel ms, setup/compaction ms, matching launches) of the last batch."""
         ms, aux, n = C.c_double(), C.c_double(), C.c_uint32()
         _check(lib().cep_last_timing(self.h, query, C.byref(ms), C.byref(aux), C.byref(n)))
+        return ms.value, aux.value, n.value
+
+    def timing_totals(self, query: int = 0, reset: bool = False):
+        """(kernel ms, setup ms, batches) summed over the batches since the last reset."""
+        ms, aux, n = C.c_double(), C.c_double(), C.c_uint64()
+        _check(lib().cep_timing_totals(self.h, query, 1 if reset else 0, C.byref(ms), C.byref(aux), C.byref(n)))
         return ms.value, aux.value, n.value
 
     def stats(self, query: int = 0) -> dict:

@@ -7,6 +7,8 @@
 #include <unistd.h>
 
 #include <cstdint>
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include QUERY_SRC
@@ -125,11 +127,14 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   if (g_bits_used) a.bhits = bits.data();
   // persistent lanes (session.cpp): one "lane" claims every job in turn; streams: lane per key
   auto launch = [&](uint64_t nslots, uint32_t rc, int df) {
-    if (!streaming) {
+    // $CEP_LANE_NO_PERSIST: one lane per job, as session.cpp launches single queries
+    if (!streaming && !std::getenv("CEP_LANE_NO_PERSIST")) {
       job_next = 0;
       a.job_next = &job_next;
       a.n_jobs = a.jobs ? a.n_jobs : jobs;
       nslots = 64;
+    } else if (!streaming && a.jobs) {
+      nslots = a.n_jobs;
     }
     std::vector<v4u> rings_batch;
     if (!streaming) {
@@ -150,7 +155,15 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       cep_nfa_jit(a);
     }
   };
+  // $CEP_LANE_POOL: node/pred pools of that many entries for the first launch (as session.cpp
+  // sizes them from the batch; the re-runs get the whole pools)
+  if (const char* e = std::getenv("CEP_LANE_POOL")) {
+    a.node_pool.cap = std::min<uint32_t>(a.node_pool.cap, (uint32_t)std::atol(e));
+    a.pred_pool.cap = std::min<uint32_t>(a.pred_pool.cap, (uint32_t)std::atol(e));
+  }
   launch(((nk + 63) / 64) * 64 * n_q, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
+  a.node_pool.cap = (uint32_t)nodes.size();
+  a.pred_pool.cap = (uint32_t)preds.size();
   *n_retried = 0;
   for (int round = 0; !streaming && n_cap > 0 && round < 8; round++) {  // session.cpp run_nfa
     std::vector<uint32_t> list;

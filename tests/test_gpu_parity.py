@@ -78,6 +78,60 @@ def test_stencil_many_short_keys():
     assert_parity(gpu_run(ir, off, [v]), oracle.run(ir, off, [v], threads=8), off)
 
 
+def range_chain(n):
+    """SEQ(S0..S{n-1}) all ONE + strict, S_i: i%4 <= v <= i%4 (the stencil's range fast path)."""
+    from kafkastreams_cep_amd import EventSchema, QueryBuilder
+    b = QueryBuilder(EventSchema({"v": "int"}))
+    for i in range(n):
+        sel = b.select(f"S{i}").where(lambda k, v, ts, s, i=i: (v.v >= i % 4) & (v.v <= i % 4))
+        b = sel.then() if i < n - 1 else sel
+    return b.build()
+
+
+def _boundary_stream(seed):
+    rng = np.random.default_rng(seed)
+    lens = ([4096, 4095, 1, 4097, 8, 7, 9, 0, 0, 4088, 3, 70000, 0, 5] + rng.integers(0, 4, 3000).tolist()
+            + [3 * 4096 - 1, 2, 6, 4096] + rng.integers(0, 70, 300).tolist() + [0, 0])
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    n = int(off[-1])
+    v = (np.arange(n) % 4).astype(np.int32)  # long runs of the chains' own pattern
+    v[rng.integers(0, n, size=n // 50)] = rng.integers(0, 4, size=n // 50)
+    return off, v
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("chain", ["range", "generic"])
+def test_stencil_key_boundaries(m, chain):
+    """Key starts at and around stencil_mask's 4096-event wave boundaries and among the 8
+    events before one, empty keys (also last), a key spanning more than 16 waves (wave_keys'
+    block path) and more than 64 keys starting in one wave (the key-offset chunk loop)."""
+    from test_native_abi import strict_chain
+    off, v = _boundary_stream(m)
+    ir = (range_chain(m) if chain == "range" else strict_chain(m)).to_ir()
+    assert N.Query(ir).kind == N.CEP_KIND_STENCIL
+    r = oracle.run(ir, off, [v], threads=8)
+    assert r["n_matches"] > 1000
+    assert_parity(gpu_run(ir, off, [v]), r, off)
+
+
+def test_stencil_pipelined_pushes():
+    """Stencil pushes return without a host sync: batches queued back to back, then the last
+    batch's results, and the device time of every batch (cep_timing_totals)."""
+    q = N.Query(W.strict_abc_query().to_ir())
+    s = N.Session(q)
+    batches = [W.generate(W.SynthConfig("t", "abc", 200 + 50 * i, 300, 0xCE90000 + 20 + i)) for i in range(20)]
+    s.timing_totals(0, reset=True)
+    for off, cols in batches:
+        s.push(off, cols)
+    ms, aux, n = s.timing_totals(0)
+    assert n == 20 and ms > 0 and aux > 0
+    off, cols = batches[-1]
+    assert_parity(session_result(s, 0, off, q.kind), oracle.run(q.ir, off, cols), off)
+    s.timing_totals(0, reset=True)
+    assert s.timing_totals(0)[2] == 0
+
+
 @pytest.mark.parametrize("tier", TIERS)
 @pytest.mark.parametrize("variant", ["readme", "test", "demo"])
 def test_cfg3_stock_small(variant, tier):

@@ -53,6 +53,19 @@ def test_lane_capacity_retry():
     lane_cpu.assert_same(g, oracle.run(ir, off, cols, threads=8), off)
 
 
+def test_lane_one_lane_per_key_small_pools(monkeypatch):
+    """session.cpp's launch for a single query: one lane per key (no job claiming), node and
+    pointer pools far below the batch's need, so most keys re-run on persistent lanes."""
+    monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
+    monkeypatch.setenv("CEP_LANE_POOL", "3000")
+    cfg = W.SynthConfig("t", "abc", 300, 400, 0xCE90000 + 2)
+    off, cols = W.generate(cfg)
+    ir = W.strict_abc_query().to_ir()
+    g = lane_cpu.run(ir, off, cols)
+    assert g["retried"] > 0
+    lane_cpu.assert_same(g, oracle.run(ir, off, cols, threads=8), off)
+
+
 @pytest.mark.parametrize("seed", range(0, 160, 8))
 def test_lane_fuzz(seed):
     q = random_query(seed)
