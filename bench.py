@@ -168,7 +168,7 @@ def _oracle():
     return oracle
 
 
-def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=False):
+def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=False, semantic=False):
     """The oracle on keys 0, every, 2*every, ... of the same stream (the numpy generator = the
     GPU generator bit for bit), every query in turn.  events/s = sample events x queries /
     oracle time.  gpu_check(off, cols) -> per-query (n_matches, checksum) on the GPU for the
@@ -179,13 +179,14 @@ def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=Fals
     n_ev = int(off[-1])
     el, n_m, want = 0.0, 0, []
     for p in queries:
-        r = oracle.run(p.to_ir(), off, cols, threads=threads)
+        r = oracle.run(p.to_ir(semantic_within=semantic), off, cols, threads=threads)
         el += r["elapsed_s"]
         n_m += r["n_matches"]
         emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
         pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
         pseq = r["pair_pos"].astype(np.uint64) - off[pk]
-        want.append((r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"])))
+        want.append((r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]),
+                     int(np.count_nonzero(r["err_code"]))))
     out = {"value": n_ev * len(queries) / el, "unit": "events/s" if len(queries) == 1 else "query-events/s",
            "cores": r["threads"], "kind": "port",
            "sample": f"{len(keys)} of {cfg.n_keys} keys (every {every}th), {n_ev} events x {len(queries)} "
@@ -197,12 +198,13 @@ def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=Fals
     return out
 
 
-def gpu_digests(queries, device):
+def gpu_digests(queries, device, semantic=False):
+    """per query (n_matches, checksum, keys with an exception) of the GPU on the CPU sample"""
     def check(off, cols):
-        qs = [N.Query(p.to_ir()) for p in queries]
+        qs = [N.Query(p.to_ir(semantic_within=semantic)) for p in queries]
         s = N.Session(qs, device=device)
         s.push(off, cols)
-        got = [s.digest(i) for i in range(len(qs))]
+        got = [s.digest(i) + (int(np.count_nonzero(s.key_errors(i)[0])),) for i in range(len(qs))]
         s.close()
         return got
     return check
@@ -261,6 +263,32 @@ def cfg4(device, stream, steps, warmup, dist, threads, cpu_every):
         cfg = W.SynthConfig("cfg4", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
         res["cpu_baseline"] = cpu_baseline(cfg, [W.any_kleene_query()], threads, cpu_every,
                                            gpu_digests([W.any_kleene_query()], device), extrapolated=True)
+    return res
+
+
+def semantic_cfg4(device, stream, ts, steps, warmup, dist, threads, cpu_every):
+    """config 4's query with its WITHIN 10 ms enforced (semantic mode,
+    Pattern.to_ir(semantic_within=True); the reference's own WITHIN never prunes).  Event
+    times are the stream's (1.6e12 + position: a key's events 1 ms apart), so a run expires
+    ten events after its start instead of accumulating (config 4's run explosion)."""
+    p = W.any_kleene_query()
+    ir = p.to_ir(semantic_within=True)
+    s = N.Session(N.Query(ir), device=device)
+    el, kms, _ = run_steps(s, stream, steps, warmup, dist, ts)
+    n_m, n_pairs, n_err = match_figures(s, 0, stream.n_keys)
+    st = s.stats(0)
+    s.close()
+    alg = 16.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m  # price, volume, ts
+    res = {"workload": f"cfg4 query, semantic WITHIN 10 ms (runs expire), {stream.n_keys} keys x ~1000 events "
+                       f"({stream.n_events} events), ts = 1.6e12 + position",
+           "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
+           "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
+           "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
+           "roofline": roofline(alg, kms, "cep_nfa_jit", "cep_nfa_jit_semantic")}
+    if cpu_every:
+        cfg = W.SynthConfig("cfg4s", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
+        res["cpu_baseline"] = cpu_baseline(cfg, [p], threads, cpu_every, gpu_digests([p], device, True),
+                                           extrapolated=True, semantic=True)
     return res
 
 
@@ -427,7 +455,7 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the JSON ingest figure")
     ap.add_argument("--ingest-keys", type=int, default=100_000, help="keys of the JSON ingest figure")
     ap.add_argument("--cfg5-keys", type=int, default=1_000_000)
-    ap.add_argument("--cfg5-batch", type=int, default=125_000, help="keys per pushed batch of config 5")
+    ap.add_argument("--cfg5-batch", type=int, default=250_000, help="keys per pushed batch of config 5")
     args = ap.parse_args()
 
     dist = Dist()
@@ -501,6 +529,9 @@ def main():
             log("cfg4")
             ok = max(1, args.steps // 5)
             out["other_configs"] = {"cfg4": cfg4(device, stream, ok, 1, dist, args.cpu_threads, 64 if cpu else 0)}
+            log("cfg4 semantic WITHIN")
+            out["other_configs"]["cfg4_semantic"] = semantic_cfg4(device, stream, ts, ok, 1, dist, args.cpu_threads,
+                                                                   64 if cpu else 0)
         sess.close()
         del stream, ts
         if one and not args.no_secondary:

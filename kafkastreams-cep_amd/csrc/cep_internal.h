@@ -26,6 +26,11 @@ struct cep_query {
   int rangeCols[2] = {0, 0};
   int nRangeCols = 0;
   int64_t rangeLo[8][2]{}, rangeHi[8][2]{};
+  // semantic WITHIN (IR v2 flag): epsilon stages keep their source stage's
+  // window, so runs expire (the reference's own WITHIN never prunes: parity mode)
+  bool semantic = false;
+  bool windowed = false;            // semantic and some stage has a window
+  int F = 2;                        // fold slots of a run record (states + the start slot)
   std::string jitSource;  // per-query NFA step policy for hipRTC (jit.cpp)
   std::shared_ptr<cep::ParsedQuery> parsed;  // the parsed chain and stage build (plan_groups)
 };

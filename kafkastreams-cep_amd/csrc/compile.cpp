@@ -238,6 +238,7 @@ struct Builder {
   struct PendingEdge { int stage, edge; MP m; };
   std::vector<PendingEdge> pending;
   std::vector<std::pair<int, const std::vector<std::pair<uint16_t, std::unique_ptr<Expr>>>*>> stageAggs;
+  std::vector<int64_t> window = std::vector<int64_t>(kMaxStages, -1);  // Stage.getWindowMs per stage
 
   int sk(uint16_t name, uint8_t type) {
     DevQuery& d = q->dev;
@@ -276,6 +277,8 @@ struct Builder {
     uint8_t currentType = mandatory ? (uint8_t)ST_NORMAL : type;                 // :72
     int st = newStage(cur.name, currentType);
     setAggs(st, cur);
+    // window = this pattern's WITHIN, else the successor's, else -1 (StatesFactory.java:121-127)
+    window[st] = cur.hasWindow ? cur.window : (succ && succ->hasWindow) ? succ->window : -1;
     if (!cur.pred) {  // new Stage.Edge(op, null, ...) -> IllegalArgumentException (Stage.java:159)
       q->info.compile_error = CEP_COMPILE_ILLEGAL_ARGUMENT;
       throw std::runtime_error("predicate cannot be null");
@@ -304,6 +307,7 @@ struct Builder {
       int w = newStage(cur.name, type);
       addEdge(w, OP_BEGIN, loop, leaf(cur.pred.get()));
       setAggs(w, cur);
+      window[w] = window[loop];
       st = w;
     }
     return st;
@@ -519,10 +523,10 @@ void usesM(const M* m, std::vector<bool>& fields, bool& ts) {
 
 static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& lits) {
   const DevQuery& d = q->dev;
-  const int F = d.n_states <= 2 ? 2 : d.n_states <= 4 ? 4 : 8;
+  const int F = q->F;
   std::vector<int> stTypes(d.state_type, d.state_type + d.n_states);
   std::vector<bool> fields(d.n_fields, false);
-  bool ts = false;
+  bool ts = q->windowed;  // semantic WITHIN compares event times
   for (auto& pe : b.pending) usesM(pe.m.get(), fields, ts);
   for (auto& sa : b.stageAggs)
     for (auto& a : *sa.second) uses(a.second.get(), fields, ts);
@@ -626,6 +630,24 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "  __device__ __forceinline__ uint32_t stage_sk(uint32_t sw) const {\n    if (sw & kRecEps) return (sw >> 8) & 0xFF;\n    switch (sw & 0xFF) {\n";
   for (uint32_t s = 0; s < d.n_stages; s++) o += "      case " + std::to_string(s) + ": return " + std::to_string(d.st[s].sk) + ";\n";
   o += "    }\n    return 0;\n  }\n";
+  if (q->windowed) {
+    // semantic WITHIN: the window of a stage key (an epsilon stage keeps its source stage's
+    // window), whether the key is BEGIN-typed (ComputationStage.isBeginState), event times
+    o += "  static constexpr uint32_t FS = " + std::to_string(d.n_states) + ";  // fold slot of the run's start event\n";
+    o += "  __device__ __forceinline__ int64_t sk_window(uint32_t sk) const {\n    switch (sk) {\n";
+    for (uint32_t k = 0; k < d.n_sk; k++) {
+      int64_t w = -1;
+      for (uint32_t s = 0; s < d.n_stages; s++)
+        if (d.st[s].sk == k) w = b.window[s];
+      o += "      case " + std::to_string(k) + ": return (int64_t)" + std::to_string(w) + "ll;\n";
+    }
+    o += "    }\n    return -1;\n  }\n";
+    uint32_t bmask = 0;
+    for (uint32_t k = 0; k < d.n_sk; k++)
+      if (d.sk_type[k] == ST_BEGIN) bmask |= 1u << k;
+    o += "  __device__ __forceinline__ bool sk_begin(uint32_t sk) const { return (" + std::to_string(bmask) + "u >> sk) & 1u; }\n";
+    o += "  __device__ __forceinline__ int64_t ts_at(uint64_t pos) const { return A.ts ? A.ts[pos] : (int64_t)pos; }\n";
+  }
   o += "  __device__ __forceinline__ uint16_t sk_name(uint32_t sk) const {\n    switch (sk) {\n";
   for (uint32_t k = 0; k < d.n_sk; k++) o += "      case " + std::to_string(k) + ": return " + std::to_string(d.sk_name[k]) + ";\n";
   o += "    }\n    return 0;\n  }\n";
@@ -722,6 +744,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       const std::string si = std::to_string(S.agg_state[a]);
       f += "      if (!((w.nm >> " + si + ") & 1u)) { fv[" + si + "] = w.v[" + si + "]; nm &= ~(1u << " + si + "); }\n";
     }
+    if (q->windowed) f += "      fv[FS] = w.v[FS];  // the branch keeps the run's start\n";
     f += "      L.set_folds(r, fv, nm);\n      o.produced++;\n";
     f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
     if (S.n_aggs) {
@@ -736,6 +759,17 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "  template <class LT>\n  __device__ __forceinline__ int step(LT& L, const Rec<F>& c) {\n";
   o += "    const Ev& ev = L.ev;\n    Fo w;\n";
   o += "    for (int s = 0; s < F; s++) w.v[s] = c.fold[s];\n    w.nm = c.nullmask;\n";
+  if (q->windowed) {
+    // semantic WITHIN (NFA.java:143-144 with the epsilon stage's window kept): a run whose start
+    // is more than the window before this event is dropped (produced 0 -> removePattern); a
+    // BEGIN-typed record restarts at this event (getFirstPatternTimestamp, NFA.java:347-349)
+    o += "    {\n      const uint32_t csk = stage_sk(c.stage);\n";
+    o += "      const bool cbeg = sk_begin(csk);\n";
+    o += "      const uint32_t start = cbeg ? L.j : (uint32_t)(uint64_t)c.fold[FS];\n";
+    o += "      if (!cbeg) {\n        const int64_t win = sk_window(csk);\n";
+    o += "        if (win != -1 && ev.ts - ts_at(L.base + start) > win) return 0;\n      }\n";
+    o += "      w.v[FS] = (int64_t)start;\n    }\n";
+  }
   o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
   o += "    if (c.stage & kRecEps) {\n      const uint32_t esk = (c.stage >> 8) & 0xFF;\n      switch (c.stage & 0xFF) {\n";
@@ -804,7 +838,11 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   In in{ir, ir + n};
   if (n < 8 || std::memcmp(ir, "CEPQ", 4) != 0) throw std::runtime_error("not a CEP query IR (magic)");
   in.p += 4;
-  if (in.get<uint32_t>() != 1) throw std::runtime_error("unsupported query IR version");
+  const uint32_t ver = in.get<uint32_t>();
+  if (ver != 1 && ver != 2) throw std::runtime_error("unsupported query IR version");
+  const uint32_t flags = ver == 2 ? in.get<uint32_t>() : 0u;  // v2: bit0 semantic WITHIN
+  if (flags & ~1u) throw std::runtime_error("unknown query IR flags");
+  q->semantic = (flags & 1u) != 0;
   DevQuery& d = q->dev;
   std::memset(&d, 0, sizeof d);
   uint16_t nf = in.get<uint16_t>();
@@ -867,6 +905,21 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
     throw;
   }
   q->info.n_stages = d.n_stages;
+  // semantic WITHIN: a run record carries its start event in one more fold slot; an epsilon
+  // stage's window is its source stage's, found by stage key (stages sharing a key must agree)
+  q->windowed = false;
+  if (q->semantic) {
+    for (uint32_t s = 0; s < d.n_stages; s++) q->windowed = q->windowed || b.window[s] >= 0;
+    for (uint32_t s = 0; s < d.n_stages; s++)
+      for (uint32_t t = 0; t < s; t++)
+        if (d.st[s].sk == d.st[t].sk && b.window[s] != b.window[t])
+          throw std::runtime_error("semantic WITHIN: stages with the same name and type carry different windows");
+  }
+  {
+    const uint32_t slots = d.n_states + (q->windowed ? 1u : 0u);
+    if (slots > 8) throw std::runtime_error("at most 7 fold states with semantic WITHIN");
+    q->F = slots <= 2 ? 2 : slots <= 4 ? 4 : 8;
+  }
 
   // bytecode: edge predicates, then folds
   q->code.clear();
@@ -904,7 +957,7 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
   // and state-free (so evaluating them everywhere cannot throw or differ), distinct names.
   // The stencil kernels are instantiated for 1..kMaxStencil stages (stencil.hip
   // launch_stencil); a longer strict chain runs on the NFA kernel.
-  bool stencil = np <= kMaxStencil;
+  bool stencil = np <= kMaxStencil && !q->windowed;  // (semantic windows: runs expire on ts)
   std::vector<int> seen;
   for (auto& p : ps) {
     if (p.card != CARD_ONE || p.strat != STRICT || !total(p.pred.get())) stencil = false;

@@ -881,12 +881,25 @@ struct Lane {
   }
 };
 
-// job index -> (query, key) job id: explicit (retries) or query-minor over the lane order
+// job index -> (query, key) job id: explicit (retries) or, over the lane order, blocks of 64
+// ranks: within a block every query in turn takes the block's 64 ranks.  Consecutive job
+// indices - the jobs one wave claims together - are then ONE query on 64 keys of similar
+// estimated work, so the lanes of a wave have walk queues of similar length (the wave-wide
+// drain lasts as long as the longest); query-minor order put a key's 64 variants, light and
+// heavy, into one wave, where the heaviest set the pace of all 64.
 __device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
   if (A.jobs) return A.jobs[idx];
   const uint32_t nq = A.n_q ? A.n_q : 1;
-  const uint64_t rank = idx / nq;
-  return (idx % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
+  const uint64_t blk = idx / (64ull * nq), in = idx % (64ull * nq);
+  uint64_t rank = blk * 64 + in % 64;
+  uint32_t qi = (uint32_t)(in / 64);
+  // the last block may hold fewer than 64 ranks: its jobs stay dense (query-major over them)
+  const uint64_t tail = A.n_keys - blk * 64;
+  if (tail < 64) {
+    rank = blk * 64 + in % tail;
+    qi = (uint32_t)(in / tail);
+  }
+  return (uint64_t)qi * A.n_keys + (A.order ? A.order[rank] : rank);
 }
 
 // Persistent lanes (per-batch sessions).  The launch has about as many lanes as fit the chip;

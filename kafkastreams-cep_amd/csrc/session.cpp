@@ -748,6 +748,9 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
   }
   auto s = std::make_unique<cep_session>();
   if (opts) s->opts = *opts;
+  for (int i = 0; i < n_queries; i++)
+    if (queries[i]->windowed && s->opts.tier != CEP_TIER_JIT)
+      return fail(CEP_E_INVALID, "semantic WITHIN runs on the JIT tier only");
   s->device = s->opts.device;
   int rc = guarded([&] {
     DeviceGuard g(s->device);
@@ -760,8 +763,7 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
     for (int i = 0; i < n_queries; i++) {
       auto r = std::make_unique<QueryRt>();
       r->q = queries[i];
-      const uint32_t ns = queries[i]->info.n_states;
-      r->F = ns <= 2 ? 2 : ns <= 4 ? 4 : 8;
+      r->F = queries[i]->F;  // fold slots of a run record (compile.cpp)
       r->d_q.ensure(sizeof(DevQuery));
       HIPCHECK(hipMemcpy(r->d_q.p, &queries[i]->dev, sizeof(DevQuery), hipMemcpyHostToDevice));
       r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());

@@ -104,7 +104,14 @@ class Pattern:
                     types[name] = _infer_fold_type(fn, p.schema)
         return order, types
 
-    def to_ir(self) -> bytes:
+    def to_ir(self, semantic_within: bool = False) -> bytes:
+        """The query as libcep IR.  semantic_within=False (parity mode, the default) keeps the
+        reference's WITHIN exactly: it never prunes, because every non-begin run sits in an
+        epsilon stage whose window is -1 (nfa/Stage.java:42-46, ComputationStage.java:98-100).
+        semantic_within=True is the SASE semantics the README states (README.md:19-28,
+        "WITHIN 1 hour"): an epsilon stage keeps the window of the stage it copies, so a run
+        whose first event is more than the window older than the current event is dropped
+        (NFA.java:143-144's check, then removePattern).  IR version 2 carries the flag."""
         chain = self.chain()
         schema = self.schema
         if schema is None:
@@ -116,7 +123,10 @@ class Pattern:
             if p.getName() not in names:
                 names.append(p.getName())
         out = bytearray(b"CEPQ")
-        out += struct.pack("<I", 1)
+        if semantic_within:
+            out += struct.pack("<II", 2, 1)  # version 2, flags bit0: semantic WITHIN
+        else:
+            out += struct.pack("<I", 1)
         out += struct.pack("<H", len(schema.names))
         for n, t in zip(schema.names, schema.types):
             out += struct.pack("<B", t) + _str(n)

@@ -120,6 +120,7 @@ struct PatternDef {
   std::vector<AggDef> aggs;
 };
 struct QueryDef {
+  bool semantic = false;  // build-only semantic WITHIN (epsilon stages keep their window)
   std::vector<int> fieldTypes;
   std::vector<int> stateTypes;
   std::vector<std::string> stateNames;
@@ -131,8 +132,10 @@ static QueryDef parseQuery(const uint8_t* ir, size_t n) {
   Reader r{ir, ir + n};
   if (n < 8 || std::memcmp(ir, "CEPQ", 4) != 0) throw std::runtime_error("bad IR magic");
   r.p += 4;
-  if (r.get<uint32_t>() != 1) throw std::runtime_error("bad IR version");
+  const uint32_t ver = r.get<uint32_t>();
+  if (ver != 1 && ver != 2) throw std::runtime_error("bad IR version");
   QueryDef q;
+  q.semantic = ver == 2 && (r.get<uint32_t>() & 1u);  // v2 flags: bit0 semantic WITHIN
   uint16_t nf = r.get<uint16_t>();
   for (int i = 0; i < nf; i++) { q.fieldTypes.push_back(r.get<uint8_t>()); r.str(); }
   uint16_t ns = r.get<uint16_t>();
@@ -197,11 +200,14 @@ struct Stage {
 };
 
 // Stage.newEpsilonState (Stage.java:42-46): name/type of `current`, single PROCEED(true) edge
-static StageP newEpsilonState(const Stage* current, Stage* target) {
+// semantic: the build's semantic-WITHIN mode (IR v2 flag, not the reference): the epsilon stage
+// also keeps `current`'s window, so ComputationStage.isOutOfWindow (:98-100) can fire
+static StageP newEpsilonState(const Stage* current, Stage* target, bool semantic) {
   if (!current) throwJ(NPE, "newEpsilonState(null)");
   auto s = std::make_shared<Stage>();
   s->name = current->name;
   s->type = current->type;
+  if (semantic) s->windowMs = current->windowMs;
   s->edges.push_back(Edge{OP_PROCEED, mTrue(), target});
   return s;
 }
@@ -710,7 +716,7 @@ struct NFA {
     bool consumed = false, ignored = false;
 
     for (auto* e : matchedEdges) {
-      StageP epsilonStage = newEpsilonState(currentStage, e->target);  // :179 (created for every edge)
+      StageP epsilonStage = newEpsilonState(currentStage, e->target, q->def.semantic);  // :179 (created for every edge)
       switch (e->op) {
         case OP_PROCEED: {
           CSP nextCS = cs;
@@ -721,7 +727,7 @@ struct NFA {
         }
         case OP_TAKE:
           if (!isBranching) {
-            StageP eps = newEpsilonState(currentStage, currentStage);
+            StageP eps = newEpsilonState(currentStage, currentStage, q->def.semantic);
             nextStages.push_back(makeCS(eps, eps.get(), version, currentEvent, startTime, sequenceID, false));
             putToSharedBuffer(currentStage, previousStage, previousEvent, currentEvent, version);
           } else {
@@ -743,7 +749,7 @@ struct NFA {
     if (isBranching) {
       int64_t newSequence = ++runs;
       int64_t latestMatchEvent = ignored ? previousEvent : currentEvent;
-      StageP eps = newEpsilonState(previousStage, currentStage);
+      StageP eps = newEpsilonState(previousStage, currentStage, q->def.semantic);
       nextStages.push_back(makeCS(eps, eps.get(), version->addRun(), latestMatchEvent, startTime, newSequence, true));
       if (!currentStage->aggregates) throwJ(NPE, "aggregates == null");
       for (auto& agg : *currentStage->aggregates) {  // ValueStore.branch :92-97

@@ -60,7 +60,7 @@ def build(ir: bytes, source: str | None = None):
     return lib
 
 
-def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None):
+def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None, ts=None):
     """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
     the batch continues the keys' streams of the previous streaming call (reset=False).
     bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the chunked scan."""
@@ -74,7 +74,8 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bit
     ptrs = (C.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
     nk = len(key_off) - 1
     retried = C.c_uint32()
-    lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None, rcap, 1 if defer else 0, C.byref(retried),
+    ts = None if ts is None else np.ascontiguousarray(ts, np.int64)
+    lib.lane_run(nk, key_off.ctypes.data, ptrs, len(cols), None if ts is None else ts.ctypes.data, rcap, 1 if defer else 0, C.byref(retried),
                  1 if streaming else 0, 1 if bits else 0, n_q, kc.ctypes.data if kc is not None and kc.size else None)
     nm, npairs = lib.lane_n_matches(), lib.lane_n_pairs()
     key = np.zeros(nm, np.uint32)

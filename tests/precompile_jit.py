@@ -17,6 +17,9 @@ def _irs(bench_only):
     irs = [W.stock_query(v).to_ir() for v in ("readme", "test", "demo")]
     irs += [W.strict_abc_query().to_ir(), W.any_kleene_query().to_ir()]
     irs += [p.to_ir() for p in W.multi_queries(64)]  # bench.py other_configs (cfg 5); tests use the first 8
+    # semantic WITHIN (tests/test_semantic_within.py, bench.py semantic figure)
+    irs += [q.to_ir(semantic_within=True) for q in (W.stock_query("readme"), W.stock_query("test"),
+                                                     W.any_kleene_query())]
     if bench_only:
         return irs
     from fuzz_queries import random_query
@@ -41,7 +44,7 @@ def _group_sets():
     mixed = [W.stock_query("readme", begin_volume=1000), W.any_kleene_query(),
              W.stock_query("readme", begin_volume=1005), W.stock_query("test"), W.stock_query("readme", dip_num=90)]
     return [[p.to_ir() for p in mq], [p.to_ir() for p in mq[48:]], [p.to_ir() for p in mq[60:]],
-            [p.to_ir() for p in mixed]]
+            [p.to_ir() for p in mixed], [p.to_ir(semantic_within=True) for p in mq[:16]]]
 
 
 def _compile_group(irs):
