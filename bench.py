@@ -455,7 +455,7 @@ def main():
     ap.add_argument("--no-ingest", action="store_true", help="skip the JSON ingest figure")
     ap.add_argument("--ingest-keys", type=int, default=100_000, help="keys of the JSON ingest figure")
     ap.add_argument("--cfg5-keys", type=int, default=1_000_000)
-    ap.add_argument("--cfg5-batch", type=int, default=250_000, help="keys per pushed batch of config 5")
+    ap.add_argument("--cfg5-batch", type=int, default=125_000, help="keys per pushed batch of config 5")
     args = ap.parse_args()
 
     dist = Dist()

@@ -301,6 +301,19 @@ int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_
                           int col_width, void* price, void* volume, int32_t* status, uint32_t* name_span,
                           void* stream);
 
+/* ---- [symbol] keying: the README query's `[symbol]` (README.md:19-28)
+ * partitions the stream by StockEvent.name.  For a batch decoded by cep_decode_stock_json with
+ * name spans: key_out[r] = index of record r's name among the batch's distinct names in order
+ * of first appearance (the name compared as the Java String deserialize() builds: UTF-16 units
+ * of the unescaped text; a null name is one symbol); records with status[r] != 0 (deserialize()
+ * throws) get 0xFFFFFFFF.  *n_symbols = distinct names.  max_symbols sizes the hash table (more
+ * distinct names fail the call).  A name holding malformed UTF-8 fails the call (CEP_E_INVALID),
+ * as does a 64-bit hash collision between different names (checked, never merged).  All
+ * arrays are device memory; n_records < 2^32; synchronous on `stream`. */
+int cep_symbol_keys(int device, const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* name_span,
+                    const int32_t* status, uint64_t n_records, uint64_t max_symbols, uint32_t* key_out,
+                    uint64_t* n_symbols, void* stream);
+
 /* ---- synthetic workloads (bench / tests): kafkastreams-cep_amd/workloads.py, on device ----
  * kind 0 = "abc" (one int column v = h % 16), 1 = "stock" (int price random walk, int volume).
  * Fills device buffers: key_off [n_keys+1] (u64), cols[0..] (int32, n_events each).

@@ -633,7 +633,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   if (q->windowed) {
     // semantic WITHIN: the window of a stage key (an epsilon stage keeps its source stage's
     // window), whether the key is BEGIN-typed (ComputationStage.isBeginState), event times
-    o += "  static constexpr uint32_t FS = " + std::to_string(d.n_states) + ";  // fold slot of the run's start event\n";
+    o += "  static constexpr uint32_t FS = " + std::to_string(d.n_states) + ";  // fold slots FS, FS+1: the run's start time (lo, hi)\n";
     o += "  __device__ __forceinline__ int64_t sk_window(uint32_t sk) const {\n    switch (sk) {\n";
     for (uint32_t k = 0; k < d.n_sk; k++) {
       int64_t w = -1;
@@ -646,7 +646,6 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     for (uint32_t k = 0; k < d.n_sk; k++)
       if (d.sk_type[k] == ST_BEGIN) bmask |= 1u << k;
     o += "  __device__ __forceinline__ bool sk_begin(uint32_t sk) const { return (" + std::to_string(bmask) + "u >> sk) & 1u; }\n";
-    o += "  __device__ __forceinline__ int64_t ts_at(uint64_t pos) const { return A.ts ? A.ts[pos] : (int64_t)pos; }\n";
   }
   o += "  __device__ __forceinline__ uint16_t sk_name(uint32_t sk) const {\n    switch (sk) {\n";
   for (uint32_t k = 0; k < d.n_sk; k++) o += "      case " + std::to_string(k) + ": return " + std::to_string(d.sk_name[k]) + ";\n";
@@ -744,7 +743,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       const std::string si = std::to_string(S.agg_state[a]);
       f += "      if (!((w.nm >> " + si + ") & 1u)) { fv[" + si + "] = w.v[" + si + "]; nm &= ~(1u << " + si + "); }\n";
     }
-    if (q->windowed) f += "      fv[FS] = w.v[FS];  // the branch keeps the run's start\n";
+    if (q->windowed) f += "      fv[FS] = w.v[FS];  // the branch keeps the run's start\n      fv[FS + 1] = w.v[FS + 1];\n";
     f += "      L.set_folds(r, fv, nm);\n      o.produced++;\n";
     f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
     if (S.n_aggs) {
@@ -765,10 +764,10 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     // BEGIN-typed record restarts at this event (getFirstPatternTimestamp, NFA.java:347-349)
     o += "    {\n      const uint32_t csk = stage_sk(c.stage);\n";
     o += "      const bool cbeg = sk_begin(csk);\n";
-    o += "      const uint32_t start = cbeg ? L.j : (uint32_t)(uint64_t)c.fold[FS];\n";
+    o += "      const int64_t start = cbeg ? ev.ts : (int64_t)(((uint64_t)(uint32_t)c.fold[FS + 1] << 32) | (uint32_t)c.fold[FS]);\n";
     o += "      if (!cbeg) {\n        const int64_t win = sk_window(csk);\n";
-    o += "        if (win != -1 && ev.ts - ts_at(L.base + start) > win) return 0;\n      }\n";
-    o += "      w.v[FS] = (int64_t)start;\n    }\n";
+    o += "        if (win != -1 && ev.ts - start > win) return 0;\n      }\n";
+    o += "      w.v[FS] = (int64_t)(uint32_t)(uint64_t)start;\n      w.v[FS + 1] = (int64_t)(uint32_t)((uint64_t)start >> 32);\n    }\n";
   }
   o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
@@ -905,7 +904,7 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
     throw;
   }
   q->info.n_stages = d.n_stages;
-  // semantic WITHIN: a run record carries its start event in one more fold slot; an epsilon
+  // semantic WITHIN: a run record carries its start time in two more fold slots; an epsilon
   // stage's window is its source stage's, found by stage key (stages sharing a key must agree)
   q->windowed = false;
   if (q->semantic) {
@@ -916,8 +915,8 @@ void compile_query(const uint8_t* ir, size_t n, cep_query* q) {
           throw std::runtime_error("semantic WITHIN: stages with the same name and type carry different windows");
   }
   {
-    const uint32_t slots = d.n_states + (q->windowed ? 1u : 0u);
-    if (slots > 8) throw std::runtime_error("at most 7 fold states with semantic WITHIN");
+    const uint32_t slots = d.n_states + (q->windowed ? 2u : 0u);
+    if (slots > 8) throw std::runtime_error("at most 6 fold states with semantic WITHIN");
     q->F = slots <= 2 ? 2 : slots <= 4 ? 4 : 8;
   }
 

@@ -39,6 +39,7 @@ struct NfaArgs {
   uint32_t* job_next;        // persistent lanes (nfa_lane.h run_jobs): next job index to claim;
                              // null: one job per lane (streaming sessions)
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
+  uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
   Node* nodes;
   Pred* preds;               // the predecessor pool (a node's second and later pointers)

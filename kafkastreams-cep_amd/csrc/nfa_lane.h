@@ -881,23 +881,21 @@ struct Lane {
   }
 };
 
-// job index -> (query, key) job id: explicit (retries) or, over the lane order, blocks of 64
-// ranks: within a block every query in turn takes the block's 64 ranks.  Consecutive job
-// indices - the jobs one wave claims together - are then ONE query on 64 keys of similar
-// estimated work, so the lanes of a wave have walk queues of similar length (the wave-wide
-// drain lasts as long as the longest); query-minor order put a key's 64 variants, light and
-// heavy, into one wave, where the heaviest set the pace of all 64.
+// job index -> (query, key) job id: explicit (retries) or query-minor over the lane order
+// (job_map 1, measurement runs: a wave = 8 queries x 8 keys of similar work, for groups of a
+// multiple of 8 queries; the tail block query-minor)
 __device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
   if (A.jobs) return A.jobs[idx];
   const uint32_t nq = A.n_q ? A.n_q : 1;
-  const uint64_t blk = idx / (64ull * nq), in = idx % (64ull * nq);
-  uint64_t rank = blk * 64 + in % 64;
-  uint32_t qi = (uint32_t)(in / 64);
-  // the last block may hold fewer than 64 ranks: its jobs stay dense (query-major over them)
-  const uint64_t tail = A.n_keys - blk * 64;
-  if (tail < 64) {
-    rank = blk * 64 + in % tail;
-    qi = (uint32_t)(in / tail);
+  uint64_t rank = idx / nq;
+  uint32_t qi = (uint32_t)(idx % nq);
+  if (A.job_map == 1 && nq % 8 == 0) {
+    const uint64_t blk = idx / (64ull * nq);
+    if ((blk + 1) * 64 <= A.n_keys) {
+      const uint64_t in = idx % (64ull * nq), w = in / 64, l = in % 64, qo = nq / 8;
+      qi = (uint32_t)((w % qo) * 8 + l % 8);
+      rank = blk * 64 + (w / qo) * 8 + l / 8;
+    }
   }
   return (uint64_t)qi * A.n_keys + (A.order ? A.order[rank] : rank);
 }

@@ -453,6 +453,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   if (persist) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
+    if (const char* e = std::getenv("CEP_JOB_MAP")) a.job_map = (uint32_t)std::atoi(e);  // (measurement runs)
   }
   if (streaming) {  // walks in place: a conflict could not be re-run (nfa_lane.h)
     a.defer = 0;
@@ -1427,6 +1428,27 @@ int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_
     HIPCHECK(launch_decode_stock_json(bytes, rec_off, n_records, col_width, price, volume, status, name_span,
                                       (hipStream_t)stream));
   });
+}
+
+int cep_symbol_keys(int device, const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* name_span,
+                    const int32_t* status, uint64_t n_records, uint64_t max_symbols, uint32_t* key_out,
+                    uint64_t* n_symbols, void* stream) {
+  if (!rec_off || !name_span || !key_out || !n_symbols || (!bytes && n_records))
+    return fail(CEP_E_INVALID, "null argument");
+  if (n_records >= 0xFFFFFFFFull) return fail(CEP_E_INVALID, "n_records must be < 2^32");
+  if (max_symbols == 0) max_symbols = n_records;
+  uint32_t err = 0;
+  int rc = guarded([&] {
+    DeviceGuard g(device);
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(symbol_keys(bytes, rec_off, name_span, status, n_records, max_symbols, key_out, n_symbols, &err,
+                         (hipStream_t)stream));
+  });
+  if (rc) return rc;
+  if (err & 1u) return fail(CEP_E_INVALID, "a record's name holds malformed UTF-8");
+  if (err & 2u) return fail(CEP_E_INVALID, "more distinct names than max_symbols");
+  if (err & 4u) return fail(CEP_E_INVALID, "64-bit hash collision between two different names");
+  return CEP_OK;
 }
 
 int cep_synth_stock_json(int device, const int32_t* price_dev, const int32_t* volume_dev, uint64_t n,

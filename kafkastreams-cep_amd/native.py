@@ -27,7 +27,7 @@ EXPORTS = [
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
     "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
-    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals",
+    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals", "cep_symbol_keys",
 ]
 
 
@@ -112,6 +112,7 @@ def lib():
             "cep_session_restore": ([vp, vp, C.c_size_t], C.c_int),
             "cep_decode_stock_json": ([C.c_int, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
             "cep_synth_stock_json": ([C.c_int, vp, vp, u64, vp, u64, vp, C.POINTER(u64)], C.c_int),
+            "cep_symbol_keys": ([C.c_int, vp, vp, vp, vp, u64, u64, vp, C.POINTER(u64), vp], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -375,6 +376,18 @@ def decode_stock_json(batch: StockJsonBatch, col_width: int = 8, out: DecodedSto
                                        out.name_span.ptr if out.name_span is not None else None, stream))
     out._src = batch  # the launch is asynchronous: keep the input's device buffers alive with the output
     return out
+
+
+def symbol_keys(batch: StockJsonBatch, decoded: DecodedStock, max_symbols: int = 0, stream=None):
+    """cep_symbol_keys: the [symbol] key of every record (index of its name in order of first
+    appearance; 0xFFFFFFFF for records whose deserialize() throws) -> (DeviceBuffer u32[n],
+    n_symbols).  `decoded` must hold name spans."""
+    assert decoded.name_span is not None and decoded.n == batch.n
+    keys = DeviceBuffer(4 * max(1, batch.n), batch.device)
+    ns = C.c_uint64()
+    _check(lib().cep_symbol_keys(batch.device, batch.data.ptr, batch.rec_off.ptr, decoded.name_span.ptr,
+                                 decoded.status.ptr, batch.n, max_symbols, keys.ptr, C.byref(ns), stream))
+    return keys, ns.value
 
 
 class Session:

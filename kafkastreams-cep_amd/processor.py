@@ -178,7 +178,10 @@ class CEPProcessor:
     """CEPProcessor.java:54-193 over a streaming libcep session (one NFA per key)."""
 
     def __init__(self, pattern, in_memory: bool = False, *, batch_size: int = 4096,
-                 max_keys: int = 1 << 16, device: int = 0, session_factory=None):
+                 max_keys: int = 1 << 16, device: int = 0, session_factory=None, semantic_within: bool = False):
+        """semantic_within: enforce the query's WITHIN on the record timestamps (this build's
+        semantic mode, Pattern.to_ir(semantic_within=True)); the default is the reference's
+        behaviour, where WITHIN never prunes."""
         self.pattern = pattern
         self.in_memory = in_memory  # the reference's store choice; device state is in HBM either way
         self.batch_size = max(1, int(batch_size))
@@ -187,7 +190,7 @@ class CEPProcessor:
         self.schema = pattern.schema
         if self.schema is None:
             raise ValueError("the pattern needs an EventSchema (QueryBuilder(schema))")
-        self.ir = pattern.to_ir()  # interns string literals before any value is encoded
+        self.ir = pattern.to_ir(semantic_within=semantic_within)  # interns string literals first
         self._session_factory = session_factory
         self.context = None
         self.session = None

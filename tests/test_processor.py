@@ -233,3 +233,23 @@ def test_interleaved_keys_forward_order_gpu(batch, punct):
 @pytest.mark.parametrize("batch", [1, 16, 1000])
 def test_key_exception_after_earlier_matches_gpu(batch):
     _check_error_run(True, batch)
+
+
+@pytest.mark.gpu
+def test_semantic_within_processor_gpu():
+    """semantic_within=True enforces the README query's WITHIN 1 hour on the record times.  1 ms
+    apart: the README's 4 matches.  15 minutes apart: the run begun at e1 (0 min) has expired
+    by e8 (105 min), so its second match goes; the run begun at e3 (30 min) still completes at
+    e8.  40 minutes apart: every run expires before its dip.  The default processor (the
+    reference's WITHIN, never pruning) gives the 4 matches whatever the spacing."""
+    recs = _readme_records()
+    r = README_LINES
+    for semantic, gap, want in [(True, 1, r), (True, 15 * 60_000, [r[0], r[1], r[3]]), (True, 40 * 60_000, []),
+                                (False, 40 * 60_000, r)]:
+        ctx = P.RecordContext("StockEvents", 0)
+        proc = P.CEPProcessor(W.stock_query("readme"), batch_size=3, max_keys=16, semantic_within=semantic)
+        proc.init(ctx)
+        for i, (k, v, _) in enumerate(recs):
+            ctx.send(k, v, T0 + i * gap)
+        proc.close()
+        assert [demo_json(s) for _, s in ctx.forwarded] == want, (semantic, gap)

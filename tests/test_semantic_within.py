@@ -49,6 +49,19 @@ def test_lane_semantic_vs_oracle(query):
     lane_cpu.assert_same(lane_cpu.run(ir, off, cols, ts=t, defer=False), r, off)
 
 
+def test_lane_semantic_streaming():
+    """A run's start time crosses batch boundaries (it is carried in the run record)."""
+    import stream_split as SS
+    off, cols, ts = stream(n_keys=200, mean=500)
+    ir = W.stock_query("readme").to_ir(semantic_within=True)
+    r = oracle.run(ir, off, cols, ts=ts, threads=8)
+    outs = []
+    for i, (ko, cs) in enumerate(SS.split(off, list(cols) + [ts], 4, seed=4)):
+        m = lane_cpu.run(ir, ko, cs[:-1], ts=cs[-1], streaming=True, reset=(i == 0), rcap=64)
+        outs.append(m)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
 def test_semantic_prunes_and_parity_mode_does_not():
     """The window decides: with wide gaps runs expire (fewer matches than parity mode); with
     event times 1 ms apart a 1 h window never expires and the semantic result equals parity."""
@@ -74,7 +87,7 @@ def test_semantic_ir_compiles_and_gates():
     q = W.stock_query("readme")
     assert q.to_ir()[4:8] == b"\x01\x00\x00\x00"
     src = N.Query(q.to_ir(semantic_within=True)).jit_source
-    assert "sk_window" in src and "ts_at" in src
+    assert "sk_window" in src and "FS + 1" in src
     assert "sk_window" not in N.Query(q.to_ir()).jit_source
 
 
