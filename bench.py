@@ -513,9 +513,12 @@ def main():
                        "parallelism": f"key-sharded x{dist.world} (Kafka DefaultPartitioner: murmur2(key) % "
                                       f"{dist.world})" if strong else f"key ranges x{dist.world}",
                        "key_errors": int(per[:, 5].sum())},
-            "roofline": roofline(alg, kms, "cep_nfa_jit", compaction_ms=aux_ms,
-                                 bitmap_sort_ms=st["kernel_ms"] - st["main_ms"] - st["retry_ms"],
-                                 main_ms=st["main_ms"]),
+            # the dominant kernel's own launch (cep_nfa_jit, HIP events around it on the session
+            # stream; rocprofv3's average for it agrees, profiles/r02/); the step's other kernels
+            # (work estimate + lane order + begin-hit bitmap, compaction) listed beside it
+            "roofline": roofline(alg, st["main_ms"], "cep_nfa_jit", step_kernels_ms=kms, compaction_ms=aux_ms,
+                                 est_order_bits_ms=st["kernel_ms"] - st["main_ms"] - st["retry_ms"],
+                                 retry_ms=st["retry_ms"]),
             "watermark": wm,
             "checksum": f"{checksum:016x}",
         }

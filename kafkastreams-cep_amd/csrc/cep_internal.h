@@ -60,6 +60,7 @@ hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_li
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
 uint64_t scatter_heavy_bytes(uint64_t n_keys);
+hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st);  // exclusive, symbol.hip
 hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* span, const int32_t* status,
                        uint64_t n, uint64_t max_symbols, uint32_t* key, uint64_t* n_symbols, uint32_t* err,
                        hipStream_t st);

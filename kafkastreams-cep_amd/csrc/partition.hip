@@ -14,6 +14,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "cep_internal.h"
 #include "kernel_args.h"
 
 namespace cep {
@@ -23,11 +24,130 @@ __global__ void __launch_bounds__(256) iota_u32(uint32_t* v, uint64_t n) {
   if (i < n) v[i] = (uint32_t)i;
 }
 
-// range check of the key ids (the sort only looks at the bits of n_keys - 1)
-__global__ void __launch_bounds__(256) check_keys(const uint32_t* __restrict__ key, uint64_t n, uint64_t n_keys,
-                                                  unsigned* bad) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n && key[i] >= n_keys) atomicOr(bad, 1u);
+// ---- stable LSD counting sort of (key, arrival index) by key, hand-written -------------
+// Digits of <= 8 bits (256 bins): a 20-bit key space (1M keys) is three passes.  Per pass:
+//   rs_hist     per tile of 8192 events, a digit histogram in LDS -> hist[bin * T + tile]
+//   scan_u32    exclusive scan of hist (bin-major, tile-minor): each (bin, tile)'s first slot
+//   rs_scatter  per tile: each wave ranks its events within their digit with ballots (one
+//               ballot per digit bit; peers = the lanes whose digits agree) and per-wave digit
+//               counters in LDS; the tile is then sorted by digit in LDS and written out bin run
+//               by bin run, so consecutive lanes store consecutive words (coalesced).
+// Stability: within a wave by round then lane, across waves by the prefix, across tiles by
+// the scan order - every key's events keep arrival order.  The first pass reads the caller's
+// key array (and range-checks it) and makes the arrival index from the position; the last
+// writes the sorted keys and the permutation.
+constexpr int kRsThreads = 256, kRsRounds = 32, kRsWaves = kRsThreads / 64;
+constexpr uint64_t kRsTile = (uint64_t)kRsThreads * kRsRounds;  // 8192 events
+constexpr int kRsMaxBits = 8;
+constexpr uint32_t kRsBins = 1u << kRsMaxBits;
+
+template <bool FIRST, bool INV>
+__global__ void __launch_bounds__(kRsThreads) rs_hist(const uint32_t* __restrict__ keys, uint64_t n, uint64_t n_keys,
+                                                      int shift, int bits, uint32_t* hist, uint64_t T, unsigned* bad) {
+  __shared__ uint32_t h[kRsBins];
+  const uint32_t bins = 1u << bits, mask = bins - 1;
+  for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) h[d] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+  bool oob = false;
+#pragma unroll 8
+  for (int r = 0; r < kRsRounds; r++) {
+    const uint64_t i = t0 + (uint64_t)r * kRsThreads + threadIdx.x;
+    if (i < n) {
+      const uint32_t k = (FIRST && INV) ? ~keys[i] : keys[i];
+      if (FIRST && !INV && k >= n_keys) oob = true;
+      atomicAdd(&h[(k >> shift) & mask], 1u);
+    }
+  }
+  if (FIRST && oob) atomicOr(bad, 1u);
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) hist[(uint64_t)d * T + blockIdx.x] = h[d];
+}
+
+template <bool FIRST, bool INV>
+__global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                         uint64_t n, int shift, int bits,
+                                                         const uint32_t* __restrict__ off, uint64_t T, uint32_t* kout,
+                                                         uint32_t* vout) {
+  __shared__ uint32_t cnt[kRsWaves][kRsBins];  // per-wave digit counts -> the waves' first local slots
+  __shared__ uint32_t lstart[kRsBins], gbase[kRsBins];
+  __shared__ uint32_t sk[kRsTile], sv[kRsTile];  // the tile sorted by digit
+  const uint32_t bins = 1u << bits, mask = bins - 1;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t d = threadIdx.x; d < kRsBins; d += kRsThreads)
+#pragma unroll
+    for (int x = 0; x < kRsWaves; x++) cnt[x][d] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+  const uint32_t tn = (uint32_t)(n - t0 < kRsTile ? n - t0 : kRsTile);
+  // this wave's events: a contiguous quarter of the tile, 64 per round
+  const uint32_t e0 = w * (uint32_t)(kRsTile / kRsWaves);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t key[kRsRounds], val[kRsRounds], rank[kRsRounds];
+#pragma unroll
+  for (int r = 0; r < kRsRounds; r++) {
+    const uint32_t i = e0 + (uint32_t)r * 64 + lane;
+    key[r] = i < tn ? ((FIRST && INV) ? ~kin[t0 + i] : kin[t0 + i]) : 0u;
+    val[r] = i < tn ? (FIRST ? (uint32_t)(t0 + i) : vin[t0 + i]) : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kRsRounds; r++) {
+    const bool valid = e0 + (uint32_t)r * 64 + lane < tn;
+    const uint32_t d = (key[r] >> shift) & mask;
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < bits; b++) {
+      const uint64_t bb = __ballot(valid && ((d >> b) & 1u));
+      peers &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    uint32_t base = 0;
+    if (valid) base = cnt[w][d];  // every lane reads before the leader writes (one wave, in order)
+    rank[r] = base + (uint32_t)__popcll(peers & lt);
+    if (valid && (peers & lt) == 0) cnt[w][d] = base + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // tile-local bin starts (exclusive scan of the bin totals, one wave), then per wave
+  if (w == 0) {
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < kRsBins; c0 += 64) {
+      const uint32_t d = c0 + lane;
+      uint32_t t = 0;
+#pragma unroll
+      for (int x = 0; x < kRsWaves; x++) t += cnt[x][d];
+      uint32_t s2 = t;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(s2, o, 64);
+        if (lane >= (uint32_t)o) s2 += y;
+      }
+      const uint32_t ex = carry + s2 - t;
+      lstart[d] = ex;
+      uint32_t run = ex;
+#pragma unroll
+      for (int x = 0; x < kRsWaves; x++) {
+        const uint32_t c = cnt[x][d];
+        cnt[x][d] = run;
+        run += c;
+      }
+      gbase[d] = d < bins ? off[(uint64_t)d * T + blockIdx.x] : 0u;
+      carry += __shfl(s2, 63, 64);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRsRounds; r++) {
+    if (e0 + (uint32_t)r * 64 + lane < tn) {
+      const uint32_t p = cnt[w][(key[r] >> shift) & mask] + rank[r];
+      sk[p] = key[r];
+      sv[p] = val[r];
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < tn; i += kRsThreads) {
+    const uint32_t k = sk[i], d = (k >> shift) & mask;
+    const uint32_t g = gbase[d] + (i - lstart[d]);
+    kout[g] = k;
+    vout[g] = sv[i];
+  }
 }
 
 // key_off[k] = first position of a key >= k in the sorted keys (binary search per key)
@@ -44,20 +164,50 @@ __global__ void __launch_bounds__(256) key_offsets(const uint32_t* __restrict__ 
   key_off[k] = lo;
 }
 
-// CSR position p <- arrival index perm[p], for every column (4- or 8-byte values) and ts
+// CSR position p <- arrival index perm[p], for every column (4- or 8-byte values) and ts.
+// The column reads are scattered (a key's events sit n_keys apart in round-robin arrival
+// order), so each thread gathers kGaPer positions with all their loads in flight at once.
+// XCD-aware: workgroups go round-robin to the 8 XCDs (block b -> XCD b % 8); block b takes
+// tile (b % 8) * per + b / 8, so each XCD walks one contiguous eighth of the CSR positions and
+// its own L2 keeps the arrival-order lines that neighbouring keys share (key k's j-th event
+// sits next to key k+1's).
+constexpr int kGaPer = 8;
 __global__ void __launch_bounds__(256) gather_cols(const uint32_t* __restrict__ perm, uint64_t n, int nf, Cols in,
                                                    Cols out, uint32_t wide_mask, const int64_t* ts_in,
-                                                   int64_t* ts_out) {
-  const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t src = perm[p];
-  for (int f = 0; f < nf; f++) {
-    if ((wide_mask >> f) & 1u)
-      ((int64_t*)out.p[f])[p] = ((const int64_t*)in.p[f])[src];
-    else
-      ((int32_t*)out.p[f])[p] = ((const int32_t*)in.p[f])[src];
+                                                   int64_t* ts_out, uint64_t per) {
+  const uint64_t tile = (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  const uint64_t p0 = tile * 256 * kGaPer + threadIdx.x;
+  uint32_t src[kGaPer];
+#pragma unroll
+  for (int k = 0; k < kGaPer; k++) {
+    const uint64_t p = p0 + (uint64_t)k * 256;
+    src[k] = p < n ? perm[p] : 0u;
   }
-  if (ts_in) ts_out[p] = ts_in[src];
+  for (int f = 0; f < nf; f++) {
+    if ((wide_mask >> f) & 1u) {
+      int64_t v[kGaPer];
+#pragma unroll
+      for (int k = 0; k < kGaPer; k++) v[k] = p0 + (uint64_t)k * 256 < n ? ((const int64_t*)in.p[f])[src[k]] : 0;
+#pragma unroll
+      for (int k = 0; k < kGaPer; k++)
+        if (p0 + (uint64_t)k * 256 < n) ((int64_t*)out.p[f])[p0 + (uint64_t)k * 256] = v[k];
+    } else {
+      int32_t v[kGaPer];
+#pragma unroll
+      for (int k = 0; k < kGaPer; k++) v[k] = p0 + (uint64_t)k * 256 < n ? ((const int32_t*)in.p[f])[src[k]] : 0;
+#pragma unroll
+      for (int k = 0; k < kGaPer; k++)
+        if (p0 + (uint64_t)k * 256 < n) ((int32_t*)out.p[f])[p0 + (uint64_t)k * 256] = v[k];
+    }
+  }
+  if (ts_in) {
+    int64_t v[kGaPer];
+#pragma unroll
+    for (int k = 0; k < kGaPer; k++) v[k] = p0 + (uint64_t)k * 256 < n ? ts_in[src[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < kGaPer; k++)
+      if (p0 + (uint64_t)k * 256 < n) ts_out[p0 + (uint64_t)k * 256] = v[k];
+  }
 }
 
 static int key_bits(uint64_t n_keys) {
@@ -66,53 +216,92 @@ static int key_bits(uint64_t n_keys) {
   return b;
 }
 
-// Device scratch of partition(): bytes needed for n events over n_keys keys.
-size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys) {
-  (void)n_keys;
-  size_t tmp = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1));
-  return tmp + 256;
+static uint64_t rs_tiles(uint64_t n) { return std::max<uint64_t>(1, (n + kRsTile - 1) / kRsTile); }
+
+// Device scratch of lsd_sort: bytes needed for n keys of `bits` bits (histograms and their
+// scan, one (key, value) ping-pong pair per intermediate pass).
+static size_t lsd_scratch_bytes(uint64_t n, int bits) {
+  const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  const uint64_t h = (uint64_t)(1u << kRsMaxBits) * rs_tiles(n);
+  const uint64_t mid = passes > 1 ? (uint64_t)(passes > 2 ? 2 : 1) * 8 * std::max<uint64_t>(n, 1) : 0;
+  return 4 * (2 * h + 256) + mid + 1024;
 }
 
+// Stable sort of n u32 keys (`bits` significant bits; inv: by ~key, i.e. descending) ->
+// sorted keys (complemented when inv) and the source index of each output position.
+// check_keys > 0: keys >= check_keys set *bad.
+static hipError_t lsd_sort(const uint32_t* key, uint64_t n, int bits, bool inv, uint64_t check_keys,
+                           uint32_t* sorted_keys, uint32_t* perm, void* scratch, size_t scratch_bytes, unsigned* bad,
+                           hipStream_t st) {
+  if (!n) return hipSuccess;
+  const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  const int width = (bits + passes - 1) / passes;
+  const uint64_t T = rs_tiles(n);
+  if (lsd_scratch_bytes(n, bits) > scratch_bytes) return hipErrorInvalidValue;
+  uint32_t* hist = (uint32_t*)scratch;
+  uint32_t* hoff = hist + ((uint64_t)1 << width) * T;
+  uint32_t* mid = (uint32_t*)((char*)scratch + 4 * (2 * (uint64_t)(1u << kRsMaxBits) * T + 256));
+  uint32_t *mk[2] = {mid, mid + 2 * n}, *mv[2] = {mid + n, mid + 3 * n};
+  const uint32_t *ik = key, *iv = nullptr;
+  const dim3 g((uint32_t)T), b(kRsThreads);
+  hipError_t e = hipSuccess;
+  for (int p = 0; p < passes; p++) {
+    const int shift = p * width, w = std::min(width, bits - shift);
+    const bool last = p == passes - 1;
+    uint32_t* ok = last ? sorted_keys : mk[p & 1];
+    uint32_t* ov = last ? perm : mv[p & 1];
+    const uint64_t nk = check_keys ? check_keys : ~0ull;
+    if (p > 0) hipLaunchKernelGGL((rs_hist<false, false>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else if (inv) hipLaunchKernelGGL((rs_hist<true, true>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else hipLaunchKernelGGL((rs_hist<true, false>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    if ((e = scan_u32(hist, hoff, ((uint64_t)1 << w) * T, st)) != hipSuccess) return e;
+    if (p > 0) hipLaunchKernelGGL((rs_scatter<false, false>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    else if (inv) hipLaunchKernelGGL((rs_scatter<true, true>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    else hipLaunchKernelGGL((rs_scatter<true, false>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    ik = ok;
+    iv = ov;
+  }
+  return hipGetLastError();
+}
+
+// Device scratch of partition(): bytes needed for n events over n_keys keys.
+size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys) { return lsd_scratch_bytes(n, key_bits(n_keys)); }
+
 // arrival-order batch -> key_off[n_keys + 1], perm[n] (arrival index of each CSR position),
-// columns in CSR order.  scratch: partition_scratch_bytes; sorted_keys, idx: n u32 each.
+// columns in CSR order.  scratch: partition_scratch_bytes; sorted_keys: n u32.
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
                      hipStream_t st) {
   (void)cnt;
-  const uint32_t blocks = (uint32_t)((n + 255) / 256);
-  hipError_t e = hipSuccess;
-  if (n) {
-    hipLaunchKernelGGL(check_keys, dim3(blocks), dim3(256), 0, st, key, n, n_keys, bad);
-    hipLaunchKernelGGL(iota_u32, dim3(blocks), dim3(256), 0, st, idx, n);
-    size_t tmp = scratch_bytes;
-    e = hipcub::DeviceRadixSort::SortPairs(scratch, tmp, key, sorted_keys, idx, perm, (int)n, 0, key_bits(n_keys), st);
-    if (e != hipSuccess) return e;
-  }
+  (void)idx;
+  hipError_t e = lsd_sort(key, n, key_bits(n_keys), false, n_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(key_offsets, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, st, sorted_keys, n, n_keys,
                      key_off);
-  if (n) hipLaunchKernelGGL(gather_cols, dim3(blocks), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in, ts_out);
+  if (n) {
+    const uint64_t tiles = (n + 256 * kGaPer - 1) / (256 * kGaPer), per = (tiles + 7) / 8;
+    hipLaunchKernelGGL(gather_cols, dim3((uint32_t)(8 * per)), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in,
+                       ts_out, per);
+  }
   return hipGetLastError();
 }
 
-// keys by estimated work, longest first (the NFA's lane order, session.cpp)
+// keys by estimated work, longest first (the NFA's lane order, session.cpp): a stable LSD sort
+// by ~est, so equal estimates keep key order
 hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
-  hipLaunchKernelGGL(iota_u32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, iota_tmp, n);
-  size_t need = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, need, est, est_sorted, iota_tmp, order, (int)n,
-                                                              0, 32, st);
-  if (e != hipSuccess) return e;
+  (void)iota_tmp;
+  const size_t need = lsd_scratch_bytes(n, 32);
   if (need > tmp_bytes) {
     if (tmp) (void)hipFree(tmp);
     tmp = nullptr;
     tmp_bytes = 0;
-    if ((e = hipMalloc(&tmp, need)) != hipSuccess) return e;
+    hipError_t e = hipMalloc(&tmp, need);
+    if (e != hipSuccess) return e;
     tmp_bytes = need;
   }
-  return hipcub::DeviceRadixSort::SortPairsDescending(tmp, need, est, est_sorted, iota_tmp, order, (int)n, 0, 32, st);
+  return lsd_sort(est, n, 32, true, 0, est_sorted, order, tmp, tmp_bytes, nullptr, st);
 }
 
 // ---- synthetic arrival order: CSR position p of key k, index j -> sort key j * n_keys + k

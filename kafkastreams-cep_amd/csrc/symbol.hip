@@ -246,7 +246,10 @@ __global__ void __launch_bounds__(256) sym_assign(const uint8_t* __restrict__ by
   }
 }
 
-// exclusive scan of n u32 in place-free form (in -> out), recursing over the tile sums
+}  // namespace
+
+// exclusive scan of n u32 (in -> out, n < 2^32 and the total too), recursing over the tile
+// sums; shared with the partition (cep_internal.h)
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
@@ -263,8 +266,6 @@ hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s
   (void)hipFreeAsync(pre, st);
   return hipGetLastError();
 }
-
-}  // namespace
 
 hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* span, const int32_t* status,
                        uint64_t n, uint64_t max_symbols, uint32_t* key, uint64_t* n_symbols, uint32_t* err_out,

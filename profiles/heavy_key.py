@@ -26,16 +26,17 @@ def main():
     ap.add_argument("--copies", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--streaming", action="store_true", help="streaming session: walks in place, a lane per key")
     args = ap.parse_args()
     cfg = W.SynthConfig("t", "stock", 1_000_000, 1000, W.CONFIGS[3].seed)
     off, cols = W.generate(cfg, np.full(args.copies, args.key))
     ir = W.multi_queries(64)[args.query].to_ir()
-    s = N.Session(N.Query(ir))
-    s.push(off, cols)
     ks = []
-    for _ in range(args.steps):
+    for _ in range(args.steps + 1):
+        s = N.Session(N.Query(ir), streaming=args.streaming, max_runs=64 if args.streaming else 0)
         s.push(off, cols)
         ks.append(s.timing(0)[0])
+    ks = ks[1:]
     m = s.matches(0)
     res = {"key": args.key, "query": args.query, "copies": args.copies, "events_per_key": int(off[1]),
            "kernel_ms": min(ks), "matches": m["n_matches"], "pairs": m["n_pairs"], "stats": s.stats(0)}
