@@ -172,6 +172,31 @@ __device__ __forceinline__ bool dw_compatible(const Dewey& a0, const Dewey& b0) 
   return ok && dw_last(a) >= dw_last(b);
 }
 
+// isCompatible (DeweyVersion.java:62-82) for versions of at most 2 RLE pairs, from plain
+// values (a pointer's first Dewey quad is exactly this): the buffer walks' common case,
+// a handful of compares instead of dw_compatible's unrolled 6-pair selects.  a = the walker,
+// b = the pointer; canonical RLE (adjacent pairs differ in value).
+__device__ __forceinline__ bool dw_compat2(uint32_t an, uint32_t alen, int32_t av0, uint32_t ac0, int32_t av1,
+                                           uint32_t ac1, uint32_t bn, uint32_t blen, int32_t bv0, uint32_t bc0,
+                                           int32_t bv1, uint32_t bc1) {
+  if (alen > blen) {  // b is a prefix of a: b's last run fits in a's run at the same position
+    if (bn > an) return false;
+    if (bn == 0) return true;
+    if (bn == 1) return av0 == bv0 && ac0 >= bc0;
+    return av0 == bv0 && ac0 == bc0 && av1 == bv1 && ac1 >= bc1;
+  }
+  if (alen != blen) return false;
+  // equal length: all digits but the last equal, then a.last >= b.last
+  const uint32_t al = an == 2 ? ac1 - 1 : ac0 - 1, bl = bn == 2 ? bc1 - 1 : bc0 - 1;  // last run, shortened
+  const uint32_t an2 = al == 0 ? an - 1 : an, bn2 = bl == 0 ? bn - 1 : bn;
+  if (an2 != bn2) return false;
+  bool ok = true;
+  if (an2 >= 1) ok = av0 == bv0 && (an == 1 ? al : ac0) == (bn == 1 ? bl : bc0);
+  if (an2 >= 2) ok = ok && av1 == bv1 && al == bl;
+  const int32_t alast = an == 2 ? av1 : av0, blast = bn == 2 ? bv1 : bv0;
+  return ok && alast >= blast;
+}
+
 // ------------------------------------------------------------------ pool allocation
 __device__ __forceinline__ uint32_t pool_take(const Pool& p, uint32_t& cur, uint32_t& end) {
   if (cur == end) {

@@ -417,9 +417,11 @@ struct Lane {
   // come back in prev / ver
   // `pre`/`pre0`/`pre1`: the two first quads of pointer `pre`, already loaded (a walk step's
   // node's first-pred slot)
+  // `pflags` (optional): the chosen pointer's flags word, as loaded
   __device__ __forceinline__ uint32_t first_compat(uint32_t head, const Dewey& walker, uint32_t& prev, Dewey& ver,
                                                    uint32_t pre = CEP_NONE, v4u pre0 = v4u{0, 0, 0, 0},
-                                                   v4u pre1 = v4u{0, 0, 0, 0}, bool* same = nullptr) {
+                                                   v4u pre1 = v4u{0, 0, 0, 0}, bool* same = nullptr,
+                                                   uint32_t* pflags = nullptr) {
     for (uint32_t p = head; p != CEP_NONE;) {
       CEP_STAT(4);
       v4u e0 = pre0, d1 = pre1;
@@ -437,7 +439,27 @@ struct Lane {
             (en < 2 || ((int32_t)d1.z == walker.v[1] && d1.w == walker.c[1]))) {
           prev = e0.x;
           *same = true;
+          if (pflags) *pflags = fl;
           return p;
+        }
+        if (en <= 2 && walker.n <= 2) {  // both short: compare straight from the quad
+          if (dw_compat2(walker.n, walker.len, walker.v[0], walker.c[0], walker.v[1], walker.c[1], en, e0.w,
+                         en >= 1 ? (int32_t)d1.x : 0, en >= 1 ? d1.y : 0u, en >= 2 ? (int32_t)d1.z : 0,
+                         en >= 2 ? d1.w : 0u)) {
+            prev = e0.x;
+            Dewey e;
+            dw_init(e, en >= 1 ? (int32_t)d1.x : 0);
+            e.n = en;
+            e.len = e0.w;
+            e.c[0] = en >= 1 ? d1.y : 0u;
+            e.v[1] = en >= 2 ? (int32_t)d1.z : 0;
+            e.c[1] = en >= 2 ? d1.w : 0u;
+            ver = dw_pin(e);
+            if (pflags) *pflags = fl;
+            return p;
+          }
+          p = nxt;
+          continue;
         }
         Dewey e;
         e.n = en;
@@ -457,6 +479,7 @@ struct Lane {
         if (dw_compatible(walker, e)) {
           prev = e0.x;
           ver = dw_pin(e);
+          if (pflags) *pflags = fl;
           return p;
         }
       }
@@ -481,6 +504,19 @@ struct Lane {
     const uint64_t a = (uint64_t)ochunk * kOutChunkWords + opos++;
     A.out[a] = w;
     return a;
+  }
+
+  // two words (a pair's event id and stage name): one chunk check, two stores
+  __device__ __forceinline__ void out_put2(uint32_t w0, uint32_t w1) {
+    if (ochunk != CEP_NONE && opos + 2 <= kOutChunkWords - 1) {
+      uint32_t* d = A.out + (uint64_t)ochunk * kOutChunkWords + opos;
+      d[0] = w0;
+      d[1] = w1;
+      opos += 2;
+      return;
+    }
+    out_put(w0);
+    out_put(w1);
   }
 
   // ---------------------------------------------------------------- walks
@@ -531,60 +567,110 @@ struct Lane {
     }
   }
 
-  // One node of a walk at node s with walker version w.  Returns false when the walk ends
-  // (or fails); s/w advance to the next node otherwise.  `wid`: the walk's id (deferred).
+  // A walk step's reads: the node and its first-pred slot, four independent 16-B loads (one
+  // memory round trip)
+  struct WalkPre {
+    v4u n0, n1, f0, f1;  // {event, refs, head, tail}, {same_next, meta, lk, -}, first pointer quads 0-1
+  };
+  // (both addresses are materialised before the first load: otherwise the compiler computes
+  // the second address into registers the first load is still writing and waits for it
+  // in between - two round trips instead of one)
+  __device__ __forceinline__ void walk_load(uint32_t s, WalkPre& P) const {
+    const v4u* na = NQ(s, 0);
+    const v4u* pa = reinterpret_cast<const v4u*>(A.preds0 + s);
+    asm volatile("" : "+v"(na), "+v"(pa));
+    typedef __attribute__((address_space(1))) const v4u gv4u;  // the pools are global memory
+    const gv4u* gn = (const gv4u*)na;
+    const gv4u* gp = (const gv4u*)pa;
+    P.n0 = gn[0];
+    P.n1 = gn[1];
+    P.f0 = gp[0];
+    P.f1 = gp[1];
+  }
+
+  // One node of a walk at node s (its quads in P) with walker version w.  Returns false when
+  // the walk ends (or fails); s/w advance to the next node otherwise, and P holds the next
+  // node's quads: they are loaded BEFORE this node's stores are issued, so the next step waits
+  // for one load round trip, not for this step's store acknowledgements as well (vmcnt counts
+  // loads and stores in issue order).  The next node is older than this one, never the same,
+  // so none of these stores can change what was prefetched.  `wid`: the walk's id (deferred).
   __device__ __forceinline__ bool walk_node(uint32_t flags, uint32_t& s, Dewey& w, uint32_t t, uint32_t wid,
-                                            uint32_t& np) {
+                                            uint32_t& np, WalkPre& P) {
     if (s == CEP_NONE) {
       walk_fail(KE_NPE, t);
       return false;
     }
     CEP_STAT(3);
     Node& n = A.nodes[s];
-    // the node and its first-pred slot: four independent loads, one round trip
-    const v4u n0 = *NQ(s, 0), n1 = *NQ(s, 1);  // {event, refs, head, tail}, {same_next, meta, lk, -}
-    const v4u f0 = *PQ(kPred0 | s, 0), f1 = *PQ(kPred0 | s, 1);
-    const uint32_t ev_s = n0.x, head = n0.z, lk = n1.z;
+    const v4u n0 = P.n0, n1 = P.n1, f0 = P.f0, f1 = P.f1;
+    const uint32_t ev_s = n0.x, head = n0.z, lk = n1.z, cur = s;
     uint32_t meta = n1.y;
     if (!(meta & 0x100)) {
       walk_fail(KE_NPE, t);
       return false;
     }
     const int32_t refs = (int32_t)n0.y;
-    int32_t left = 1;
+    int32_t left = 1, nrefs;
+    bool del = false;
     if (flags & kWalkBranch) {
-      n.refs = refs + 1;
+      nrefs = refs + 1;
     } else {
       left = refs == 0 ? 0 : refs - 1;
-      n.refs = left;
+      nrefs = left;
       if (left == 0 && (meta >> 16) <= 1) {  // store.delete
         if (A.defer && lk > wid) {          // a put() after this walk found the node live
           walk_fail(KE_CONFLICT, t);
           return false;
         }
-        meta &= ~0x100u;
-        n.meta = meta;
-      }
-      if (flags & kWalkEmit) {
-        out_put(ev_s);
-        out_put(q.sk_name(meta & 0xFF));
-        np++;
-        if (err) {
-          walk_fail(err, t);
-          return false;
-        }
+        del = true;
       }
     }
-    uint32_t nx = CEP_NONE;
+    uint32_t nx = CEP_NONE, pfl = 0, p;
     Dewey nv;
     bool same = false;
-    const uint32_t p = first_compat(head, w, nx, nv, kPred0 | s, f0, f1, &same);
-    if (p == CEP_NONE) return false;
-    if (left == 0) {  // removePredecessor(pointer)
-      PR(p).flags |= 1u;
-      n.meta = meta - (1u << 16);
+    const uint32_t en = (f0.z >> 8) & 0xFF;
+    const int32_t bv0 = en >= 1 ? (int32_t)f1.x : 0, bv1 = en >= 2 ? (int32_t)f1.z : 0;
+    const uint32_t bc0 = en >= 1 ? f1.y : 0u, bc1 = en >= 2 ? f1.w : 0u;
+    bool fast = head == (kPred0 | cur) && !(f0.z & 1u) && en <= 2 && w.n <= 2;
+    same = fast && en == w.n && f0.w == w.len && (en < 1 || (bv0 == w.v[0] && bc0 == w.c[0])) &&
+           (en < 2 || (bv1 == w.v[1] && bc1 == w.c[1]));
+    if (fast && !same) fast = dw_compat2(w.n, w.len, w.v[0], w.c[0], w.v[1], w.c[1], en, f0.w, bv0, bc0, bv1, bc1);
+    if (fast) {
+      // the common step, straight-line: the node's first pointer is live and carries the
+      // walker's own version (a run's chain) or a compatible short one - first_compat's
+      // answer without its loop
+      p = kPred0 | cur;
+      nx = f0.x;
+      pfl = f0.z;
+      if (!same) {
+        dw_init(nv, bv0);
+        nv.n = en;
+        nv.len = f0.w;
+        nv.c[0] = bc0;
+        nv.v[1] = bv1;
+        nv.c[1] = bc1;
+      }
+    } else {
+      p = first_compat(head, w, nx, nv, kPred0 | cur, f0, f1, &same, &pfl);
     }
-    if (nx == CEP_NONE) return false;
+    const bool more = p != CEP_NONE && nx != CEP_NONE;
+    if (more) walk_load(nx, P);  // the next step's reads, ahead of this step's stores
+    n.refs = nrefs;
+    if (del) meta &= ~0x100u;
+    if (p != CEP_NONE && left == 0) {  // removePredecessor(pointer)
+      PR(p).flags = pfl | 1u;
+      meta -= 1u << 16;
+    }
+    if (del || (p != CEP_NONE && left == 0)) n.meta = meta;
+    if (!(flags & kWalkBranch) && (flags & kWalkEmit)) {
+      out_put2(ev_s, q.sk_name(meta & 0xFF));
+      np++;
+      if (err) {
+        walk_fail(err, t);
+        return false;
+      }
+    }
+    if (!more) return false;
     if (!same) w = nv;  // a value, not a pointer into the pool
     s = nx;
     return true;
@@ -624,7 +710,9 @@ struct Lane {
     uint64_t npa = 0;
     if (!walk_start(flags, sk, ev, first, t, s, npa, np)) return;
     Dewey w = dw_pin(v);
-    while (walk_node(flags, s, w, t, 0, np)) {
+    WalkPre P;
+    if (s != CEP_NONE) walk_load(s, P);
+    while (walk_node(flags, s, w, t, 0, np, P)) {
     }
     if (!err) walk_end(flags, npa, np);
   }
@@ -638,6 +726,7 @@ struct Lane {
     uint64_t npa = 0;
     Dewey w;
     dw_init(w, 0);
+    WalkPre P;
     bool active = false;
     for (;;) {
       if (!active) {
@@ -661,10 +750,11 @@ struct Lane {
         t = reinterpret_cast<const uint32_t*>(WQ(i, kWalkQuads - 1))[0];
         i++;
         if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
+        if (s != CEP_NONE) walk_load(s, P);
         active = true;
       }
       CEP_STAT(7);
-      if (!walk_node(flags, s, w, t, id0 + i - 1, np)) {
+      if (!walk_node(flags, s, w, t, id0 + i - 1, np, P)) {
         if (err) break;
         walk_end(flags, npa, np);
         active = false;

@@ -32,8 +32,12 @@ def main():
     off, cols = W.generate(cfg, np.full(args.copies, args.key))
     ir = W.multi_queries(64)[args.query].to_ir()
     ks = []
+    s = None
     for _ in range(args.steps + 1):
-        s = N.Session(N.Query(ir), streaming=args.streaming, max_runs=64 if args.streaming else 0)
+        # a streaming session continues its keys: a fresh one per step; a per-batch session is
+        # reused (its pools sized from the warm-up batch, as in a steady stream of batches)
+        if s is None or args.streaming:
+            s = N.Session(N.Query(ir), streaming=args.streaming, max_runs=64 if args.streaming else 0)
         s.push(off, cols)
         ks.append(s.timing(0)[0])
     ks = ks[1:]

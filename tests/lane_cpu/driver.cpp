@@ -85,7 +85,10 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   std::vector<Node>& nodes = *nodes_p;
   std::vector<Pred>& preds = *preds_p;
   std::vector<Pred>& preds0 = *preds0_p;
-  std::vector<uint32_t> out((ne + nk * 4 + 64) * 2 * kOutChunkWords);
+  // ($CEP_LANE_OUT_CHUNKS: a bigger output pool, for keys emitting more than ~2 pairs per event)
+  uint64_t out_chunks = (ne + nk * 4 + 64) * 2;
+  if (const char* e = std::getenv("CEP_LANE_OUT_CHUNKS")) out_chunks = std::max<uint64_t>(out_chunks, std::atoll(e));
+  std::vector<uint32_t> out(out_chunks * kOutChunkWords);
   if (n_q == 0) n_q = 1;
   const uint64_t jobs = (uint64_t)n_q * nk;
   std::vector<KeyState> ks(jobs);

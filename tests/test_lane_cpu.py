@@ -3,6 +3,8 @@ tests/lane_cpu.py, against the oracle: reference KATs, the stock configs at smal
 random fuzz queries, with walks deferred (the kernel's default) and in place (the retry
 path).  No GPU: this pins the per-event logic and the deferred-walk machinery on CPU; the
 GPU parity tests (test_gpu_parity.py) run the same code on the device."""
+import os
+
 import numpy as np
 import pytest
 
@@ -129,3 +131,16 @@ def test_lane_query_group():
     small = lane_cpu.run_group(irs[56:64], off, cols, rcap=2)
     for ir, g in zip(irs[56:64], small):
         lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+
+
+def test_dewey_short_compat_matches_general():
+    """dewey.h dw_compat2 (the buffer walks' 2-pair fast path) equals dw_compatible on every
+    pair of canonical versions of at most 2 RLE pairs over small digits."""
+    import subprocess
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = os.path.join(tempfile.mkdtemp(), "dewey_check")
+    subprocess.check_call([lane_cpu.CLANG, "-x", "c++", "-std=c++17", "-O1", "-w", f"-I{os.path.join(here, 'lane_cpu')}",
+                           f"-I{lane_cpu.CSRC}", os.path.join(here, "lane_cpu", "dewey_check.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    assert out.strip().endswith("bad 0") and "checked 14400" in out
