@@ -537,6 +537,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
+  if (lits.param) o += "#define CEP_WALK_COMPAT2 1  // kernel group: the wider straight-line walk step\n";
   o += "#include \"dewey.h\"\n#include \"java.h\"\n#include \"nfa_lane.h\"\n\nnamespace cep {\nnamespace {\n\n";
   o += "constexpr int F = " + std::to_string(F) + ";\n";
   o += "struct Ev {\n";

@@ -88,6 +88,9 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_JOB_DRAIN
 #define CEP_JOB_DRAIN 1
 #endif
+#ifndef CEP_WALK_COMPAT2
+#define CEP_WALK_COMPAT2 0
+#endif
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
 constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
@@ -588,20 +591,21 @@ struct Lane {
     P.f1 = gp[1];
   }
 
-  // One node of a walk at node s (its quads in P) with walker version w.  Returns false when
-  // the walk ends (or fails); s/w advance to the next node otherwise, and P holds the next
-  // node's quads: they are loaded BEFORE this node's stores are issued, so the next step waits
-  // for one load round trip, not for this step's store acknowledgements as well (vmcnt counts
-  // loads and stores in issue order).  The next node is older than this one, never the same,
-  // so none of these stores can change what was prefetched.  `wid`: the walk's id (deferred).
+  // One node of a walk at node s with walker version w.  Returns false when the walk ends (or
+  // fails); s/w advance to the next node otherwise.  `wid`: the walk's id (deferred).
+  // (Prefetching the next node ahead of this step's stores was measured: 4 % on the heavy
+  // walk bench, but 16 more live VGPRs across the drain loop cost cfg 3's kernel 11 % in
+  // spills; the step loads its own node.)
   __device__ __forceinline__ bool walk_node(uint32_t flags, uint32_t& s, Dewey& w, uint32_t t, uint32_t wid,
-                                            uint32_t& np, WalkPre& P) {
+                                            uint32_t& np) {
     if (s == CEP_NONE) {
       walk_fail(KE_NPE, t);
       return false;
     }
     CEP_STAT(3);
     Node& n = A.nodes[s];
+    WalkPre P;
+    walk_load(s, P);
     const v4u n0 = P.n0, n1 = P.n1, f0 = P.f0, f1 = P.f1;
     const uint32_t ev_s = n0.x, head = n0.z, lk = n1.z, cur = s;
     uint32_t meta = n1.y;
@@ -631,30 +635,39 @@ struct Lane {
     const uint32_t en = (f0.z >> 8) & 0xFF;
     const int32_t bv0 = en >= 1 ? (int32_t)f1.x : 0, bv1 = en >= 2 ? (int32_t)f1.z : 0;
     const uint32_t bc0 = en >= 1 ? f1.y : 0u, bc1 = en >= 2 ? f1.w : 0u;
+#if CEP_WALK_COMPAT2
+    // kernel groups (config 5: walk-heavy jobs): any compatible short version of the first
+    // pointer takes the straight-line step
     bool fast = head == (kPred0 | cur) && !(f0.z & 1u) && en <= 2 && w.n <= 2;
     same = fast && en == w.n && f0.w == w.len && (en < 1 || (bv0 == w.v[0] && bc0 == w.c[0])) &&
            (en < 2 || (bv1 == w.v[1] && bc1 == w.c[1]));
     if (fast && !same) fast = dw_compat2(w.n, w.len, w.v[0], w.c[0], w.v[1], w.c[1], en, f0.w, bv0, bc0, bv1, bc1);
+    if (fast && !same) {
+      dw_init(nv, bv0);
+      nv.n = en;
+      nv.len = f0.w;
+      nv.c[0] = bc0;
+      nv.v[1] = bv1;
+      nv.c[1] = bc1;
+    }
+#else
+    // single queries: only the exact version (fewer live registers in the drain loop: the
+    // wider test cost cfg 3's kernel ~11 % in spills)
+    same = head == (kPred0 | cur) && !(f0.z & 1u) && en <= 2 && en == w.n && f0.w == w.len &&
+           (en < 1 || (bv0 == w.v[0] && bc0 == w.c[0])) && (en < 2 || (bv1 == w.v[1] && bc1 == w.c[1]));
+    const bool fast = same;
+#endif
     if (fast) {
       // the common step, straight-line: the node's first pointer is live and carries the
-      // walker's own version (a run's chain) or a compatible short one - first_compat's
-      // answer without its loop
+      // walker's own version (a run's chain) - first_compat's answer without its loop
+      // (first_compat compares other short versions from the quad, dw_compat2)
       p = kPred0 | cur;
       nx = f0.x;
       pfl = f0.z;
-      if (!same) {
-        dw_init(nv, bv0);
-        nv.n = en;
-        nv.len = f0.w;
-        nv.c[0] = bc0;
-        nv.v[1] = bv1;
-        nv.c[1] = bc1;
-      }
     } else {
       p = first_compat(head, w, nx, nv, kPred0 | cur, f0, f1, &same, &pfl);
     }
     const bool more = p != CEP_NONE && nx != CEP_NONE;
-    if (more) walk_load(nx, P);  // the next step's reads, ahead of this step's stores
     n.refs = nrefs;
     if (del) meta &= ~0x100u;
     if (p != CEP_NONE && left == 0) {  // removePredecessor(pointer)
@@ -710,9 +723,7 @@ struct Lane {
     uint64_t npa = 0;
     if (!walk_start(flags, sk, ev, first, t, s, npa, np)) return;
     Dewey w = dw_pin(v);
-    WalkPre P;
-    if (s != CEP_NONE) walk_load(s, P);
-    while (walk_node(flags, s, w, t, 0, np, P)) {
+    while (walk_node(flags, s, w, t, 0, np)) {
     }
     if (!err) walk_end(flags, npa, np);
   }
@@ -726,7 +737,6 @@ struct Lane {
     uint64_t npa = 0;
     Dewey w;
     dw_init(w, 0);
-    WalkPre P;
     bool active = false;
     for (;;) {
       if (!active) {
@@ -750,11 +760,10 @@ struct Lane {
         t = reinterpret_cast<const uint32_t*>(WQ(i, kWalkQuads - 1))[0];
         i++;
         if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
-        if (s != CEP_NONE) walk_load(s, P);
         active = true;
       }
       CEP_STAT(7);
-      if (!walk_node(flags, s, w, t, id0 + i - 1, np, P)) {
+      if (!walk_node(flags, s, w, t, id0 + i - 1, np)) {
         if (err) break;
         walk_end(flags, npa, np);
         active = false;
