@@ -417,9 +417,20 @@ __global__ void __launch_bounds__(256) collect_retry(const KeyState* ks, uint64_
   else if (e == KE_CONFLICT) conf_list[atomicAdd(counts + 1, 1u)] = (uint32_t)i;
 }
 
-// One wave per heavy key: the chain is read a whole 1 KiB chunk per wave load (each lane
-// 16 B), the next chunk's load issued before the current one is parsed; the parse runs
-// wave-uniformly on words broadcast from their lanes, lane 0 storing.
+// One wave per heavy key: the chain is read a whole 1 KiB chunk per wave load (each lane 16 B =
+// chunk words 4 lane .. 4 lane + 3), the next chunk's load issued before the current one is
+// parsed.  The parse walks the chunk by SEGMENTS, wave-uniformly: a run of pair words (seq,
+// stage, seq, ...) is written by all lanes at once, each lane its own words (their pair index
+// follows from the segment's start), and only the match headers [emit, n_pairs] are read one
+// word at a time (broadcast from their lane).  A heavy key's matches are long (hundreds of
+// pairs), so most chunks are one segment: the old word-by-word parse cost ~255 dependent steps
+// per chunk (config 5's heavy variants spent ~2.5 s per 125k-key batch there).
+__device__ __forceinline__ uint32_t chunk_word(const uint4& cur, uint32_t i) {
+  const uint32_t c = i & 3;
+  const uint32_t v = c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;  // uniform select
+  return __shfl(v, (int)(i >> 2), 64);
+}
+
 __global__ void __launch_bounds__(256) scatter_heavy(const KeyState* ks, const HeavyKey* heavy, const uint32_t* n_heavy,
                                                      const uint32_t* out, uint32_t* m_key, uint32_t* m_emit,
                                                      uint64_t* m_off, uint32_t* p_seq, uint16_t* p_stage) {
@@ -428,43 +439,59 @@ __global__ void __launch_bounds__(256) scatter_heavy(const KeyState* ks, const H
   for (uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6); h < nh; h += gridDim.x * 4) {
     const HeavyKey hk = heavy[h];
     const KeyState st = ks[hk.key];
-    uint64_t mo = hk.mo, po = hk.po;
+    uint64_t mo = hk.mo;
+    uint64_t pn = hk.po;  // the pair whose seq word comes next (or, after an odd count, is open)
     uint64_t words = 2ull * st.n_matches + 2ull * st.n_pairs;  // [emit, np, (seq, stage) x np] per match
     uint32_t chunk = st.out_first;
     uint4 cur = reinterpret_cast<const uint4*>(out + (uint64_t)chunk * kOutChunkWords)[lane];
-    int state = 0;  // 0 emit, 1 np, 2 seq, 3 stage
-    uint32_t rem = 0, seq = 0;
+    int hdr = 0;        // header words still expected: 0 emit next (when rem == 0), 1 np next
+    uint64_t rem = 0;   // pair words left in the current match
     while (words) {
       const uint32_t link = __shfl(cur.w, 63, 64);  // word 255
       const uint32_t here = words > kOutChunkWords - 1 ? kOutChunkWords - 1 : (uint32_t)words;
       uint4 nxt = cur;
       if (words > here) nxt = reinterpret_cast<const uint4*>(out + (uint64_t)link * kOutChunkWords)[lane];
-      for (uint32_t i = 0; i < here; i++) {
-        const uint32_t src = i >> 2, c = i & 3;
-        const uint32_t v = c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;
-        const uint32_t w = __shfl(v, src, 64);  // every lane holds the same (c): uniform select
-        if (state == 0) {
-          if (lane == 0) {
-            m_key[mo] = hk.key;
-            m_emit[mo] = w;
-            m_off[mo] = po;
+      uint32_t p = 0;
+      while (p < here) {
+        if (rem == 0) {  // a header word
+          const uint32_t w = chunk_word(cur, p);
+          if (hdr == 0) {
+            if (lane == 0) {
+              m_key[mo] = hk.key;
+              m_emit[mo] = w;
+              m_off[mo] = pn;
+            }
+            mo++;
+            hdr = 1;
+          } else {
+            rem = 2ull * w;
+            hdr = 0;
           }
-          mo++;
-          state = 1;
-        } else if (state == 1) {
-          rem = w;
-          state = rem ? 2 : 0;
-        } else if (state == 2) {
-          seq = w;
-          state = 3;
-        } else {
-          if (lane == 0) {
-            p_seq[po] = seq;
-            p_stage[po] = (uint16_t)w;
-          }
-          po++;
-          state = --rem ? 2 : 0;
+          p++;
+          continue;
         }
+        // a segment of pair words: chunk words [p, p + len)
+        const uint32_t len = (uint32_t)(rem < (uint64_t)(here - p) ? rem : (uint64_t)(here - p));
+        const uint32_t odd = (uint32_t)(rem & 1);  // the segment starts with a stage word (its seq was earlier)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const uint32_t i = lane * 4 + c;
+          if (i >= p && i < p + len) {
+            const uint32_t v = c == 0 ? cur.x : c == 1 ? cur.y : c == 2 ? cur.z : cur.w;
+            const uint32_t d = i - p;
+            if (odd && d == 0) {
+              p_stage[pn - 1] = (uint16_t)v;
+            } else {
+              const uint32_t e = d - odd;
+              const uint64_t pair = pn + (e >> 1);
+              if (e & 1) p_stage[pair] = (uint16_t)v;
+              else p_seq[pair] = v;
+            }
+          }
+        }
+        pn += (len - odd + 1) >> 1;  // the seq words of the segment open their pairs
+        rem -= len;
+        p += len;
       }
       words -= here;
       cur = nxt;
