@@ -162,6 +162,7 @@ struct Lane {
   uint32_t n_final = 0;                      // finals queued at this event
   uint32_t ncur = 0, nend = 0, pcur = 0, pend = 0;
   uint32_t ochunk = CEP_NONE, opos = 0;
+  uint32_t ocur = 0, oend = 0;  // output chunks in hand (kept across the jobs of a persistent lane)
   uint32_t cur_first = CEP_NONE;  // node chain of event j
   int err = KE_OK;
   uint32_t err_seq = 0;
@@ -494,8 +495,11 @@ struct Lane {
   // ---------------------------------------------------------------- output stream
   __device__ __forceinline__ uint64_t out_put(uint32_t w) {
     if (ochunk == CEP_NONE || opos == kOutChunkWords - 1) {
-      const uint32_t c = atomicAdd(A.out_pool.top, 1u);
-      if (c >= A.out_pool.cap) {
+      // chunks come from the lane's range in hand, refilled A.out_pool.chunk at a time: one
+      // atomic on the pool's single counter per range (a chunk per atomic serialised ~26M
+      // same-address atomics per config-5 batch)
+      const uint32_t c = pool_take(A.out_pool, ocur, oend);
+      if (c == CEP_NONE) {
         err = KE_RETRY;
         return 0;
       }
@@ -1019,15 +1023,26 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   bool has = false, drained = false;
   int phase = 0;  // 0 events, 1 final drain pending, 2 done
   uint64_t job = 0;
+  // the wave's claimed job indices [wnext, wend) (wave-uniform): one atomic on the launch's
+  // single counter per kClaim jobs instead of one per claiming round (lanes finish jobs one
+  // at a time, so rounds mostly hand out a single job)
+  constexpr uint32_t kClaim = 128;
+  uint64_t wnext = 0, wend = 0;
   for (;;) {
     const uint64_t need = __ballot(!has && !drained);
     if (need) {
-      const int leader = __ffsll((unsigned long long)need) - 1;
-      uint32_t first = 0;
-      if ((int)lane == leader) first = atomicAdd(A.job_next, (uint32_t)__popcll(need));
-      first = __shfl(first, leader, 64);
-      if (!has && !drained) {
-        const uint64_t idx = first + (uint64_t)__popcll(need & ((1ull << lane) - 1ull));
+      if (wnext == wend) {
+        const int leader = __ffsll((unsigned long long)need) - 1;
+        uint32_t first = 0;
+        if ((int)lane == leader) first = atomicAdd(A.job_next, kClaim);
+        wnext = __shfl(first, leader, 64);
+        wend = wnext + kClaim;
+      }
+      const uint32_t cnt = (uint32_t)__popcll(need);
+      const uint32_t take = (uint64_t)cnt < wend - wnext ? cnt : (uint32_t)(wend - wnext);
+      const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+      if (!has && !drained && rank < take) {  // the others take theirs at the next round
+        const uint64_t idx = wnext + rank;
         if (idx < A.n_jobs) {
           job = job_id(A, idx);
           q.set_query((uint32_t)(job / A.n_keys));
@@ -1038,6 +1053,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
           drained = true;
         }
       }
+      wnext += take;
     }
     if (!__any(has)) break;
     // drain when a queue is long, when kJobDrain lanes wait for their final drain, or when no

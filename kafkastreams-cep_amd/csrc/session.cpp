@@ -371,12 +371,18 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // Pools: nodes / preds / output chunks, shared by the group's jobs.  Sized from the last
   // batch's use when there is one (x1.5), else from pool_factor per event and query; a job
   // that runs out is re-run below with grown pools.
-  const uint32_t nchunk = 16, pchunk = 16;
+  // per-lane pool ranges: one atomic per range on each pool's counter.  Per-batch launches
+  // (persistent lanes keep their ranges across jobs) take bigger ranges; streams hold a range
+  // per key between batches, so theirs stay small
+  const uint32_t nchunk = streaming ? 16 : 64, pchunk = nchunk, ochunk = streaming ? 1 : 8;
   const uint64_t ev_q = (uint64_t)((double)s->n_events * (double)Q);
   uint64_t node_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_nodes * 3 / 2 + 4096);
   uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_preds * 3 / 2 + 4096);
   uint64_t out_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q * 2 / kOutChunkWords) + jobs / 64 + 1024,
                                         g.last_out * 3 / 2 + 1024);
+  node_cap += slots * nchunk;  // ranges in hand at the end of the launch
+  pred_cap += slots * pchunk;
+  out_cap += slots * ochunk;
   node_cap = std::min<uint64_t>(node_cap, kNodeMax);
   pred_cap = std::min<uint64_t>(pred_cap, kNodeMax);
   out_cap = std::min<uint64_t>(out_cap, kPoolMax);  // chunk ids are u32, word addresses u64
@@ -446,7 +452,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.out = s->out.as<uint32_t>();
   a.node_pool = Pool{&sc->node_top, (uint32_t)node_cap, nchunk};
   a.pred_pool = Pool{&sc->pred_top, (uint32_t)pred_cap, pchunk};
-  a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, 1};
+  a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, ochunk};
   a.ks = g.ks.as<KeyState>();
   a.n_capacity_err = &sc->n_cap_err;
   a.n_events = s->n_events;
@@ -525,7 +531,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     HIPCHECK(launch_collect_retry(g.ks.as<KeyState>(), jobs, cap_list, conf_list, &sc->n_retry_cap, s->stream));
     // grow every pool a job ran out of (indices of the used prefix stay valid)
     const bool node_full = h.node_top >= node_cap - nchunk, pred_full = h.pred_top >= pred_cap - pchunk;
-    const bool out_full = h.out_top >= out_cap;
+    const bool out_full = (uint64_t)h.out_top + ochunk > out_cap;
     const uint64_t nn = node_full ? std::min<uint64_t>(node_cap * 4 + nlist * 64, kNodeMax) : node_cap;
     const uint64_t pn = pred_full ? std::min<uint64_t>(pred_cap * 4 + nlist * 64, kNodeMax) : pred_cap;
     const uint64_t on = out_full ? std::min<uint64_t>(out_cap * 4 + nlist, kPoolMax) : out_cap;
