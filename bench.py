@@ -483,6 +483,7 @@ def main():
     log(f"cfg3: {1e3 * el / args.steps:.2f} ms per step")
     n_m, n_pairs, n_err = match_figures(sess, 0, stream.n_keys)
     st = sess.stats(0)
+    bal_ordered, bal_identity = sess.lane_balance(0)
     digest = global_digest(sess, key_ids)
     wm = dist.min_i64(sess.watermark())
     per = dist.gather([stream.n_events, n_m, n_pairs, el, kms, float(n_err), stream.n_keys])
@@ -519,6 +520,9 @@ def main():
             "roofline": roofline(alg, st["main_ms"], "cep_nfa_jit", step_kernels_ms=kms, compaction_ms=aux_ms,
                                  est_order_bits_ms=st["kernel_ms"] - st["main_ms"] - st["retry_ms"],
                                  retry_ms=st["retry_ms"]),
+            # north_star's wave divergence figure: sum over 64-lane waves of the busiest lane's
+            # work estimate / the mean lane's, in the launch's lane order and in key order
+            "lane_balance": {"wave_max_over_mean": bal_ordered, "without_lane_order": bal_identity},
             "watermark": wm,
             "checksum": f"{checksum:016x}",
         }

@@ -259,6 +259,16 @@ typedef struct {
 } cep_batch_stats;
 int cep_last_stats(cep_session* s, int query, cep_batch_stats* out);
 
+/* Lane-work balance of the last batch's NFA launch for query `query`'s group (north_star's
+ * wave divergence figure): the per-key work estimate of cep_nfa_est (run-steps if every run
+ * lived to the end) over waves of 64 consecutive lanes; a wave lasts as long as its busiest
+ * lane, so sum over waves of (max / mean) tells how much of the launch is lane idling.
+ * *ordered: sum_waves max / sum_waves mean in the launch's longest-first lane order;
+ * *identity: the same for keys in index order (no lane order).  1.0 = perfectly balanced.
+ * Computed on demand from the last batch (a 4-B-per-key download); CEP_E_INVALID when the
+ * batch ran no estimate (stencil queries, streams, <= 64 keys). */
+int cep_lane_balance(cep_session* s, int query, double* ordered, double* identity);
+
 /* A shard of a device-resident CSR batch (multi-GPU key sharding): the events of the keys
  * sel_keys[0..n_sel) (indices into src_key_off) gathered into dst columns at dst_key_off
  * (the shard's own CSR offsets, [n_sel + 1]).  All arrays are device memory except the

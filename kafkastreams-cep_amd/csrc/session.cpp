@@ -156,6 +156,7 @@ struct GroupRt {
   DBuf kc;  // literal table, Q x nkc
   DBuf ks;  // KeyState[Q x n_keys]
   DBuf est, order, order_tmp, est_sorted;
+  bool est_valid = false;  // the last batch ran cep_nfa_est + the lane order (cep_lane_balance)
   void* sort_tmp = nullptr;  // lane-order sort scratch
   size_t sort_tmp_bytes = 0;
   // pool use of the last batch (the next batch's pools are sized from it)
@@ -488,6 +489,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
     HIPCHECK(sort_keys_by_work(g.est.as<uint32_t>(), g.est_sorted.as<uint32_t>(), g.order_tmp.as<uint32_t>(),
                                g.order.as<uint32_t>(), nk, g.sort_tmp, g.sort_tmp_bytes, s->stream));
     a.order = g.order.as<uint32_t>();
+    g.est_valid = true;
+  } else {
+    g.est_valid = false;
   }
   if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
     s->bhits.ensure(8 * ((s->n_events + 63) / 64));
@@ -1303,6 +1307,40 @@ int cep_last_stats(cep_session* s, int query, cep_batch_stats* out) {
     }
     *out = s->groups[r.group]->stats;
     out->group = (uint32_t)r.group;
+  });
+}
+
+int cep_lane_balance(cep_session* s, int query, double* ordered, double* identity) {
+  if (!s || !ordered || !identity || query < 0 || query >= (int)s->qs.size())
+    return fail(CEP_E_INVALID, "bad argument");
+  const QueryRt& r = *s->qs[query];
+  if (r.group < 0) return fail(CEP_E_INVALID, "a stencil query has no lane order");
+  GroupRt& g = *s->groups[r.group];
+  const uint64_t nk = s->n_keys;
+  if (!g.est_valid || nk <= 64 || g.est.bytes < 4 * nk) return fail(CEP_E_INVALID, "the last batch ran no work estimate");
+  return guarded([&] {
+    DeviceGuard dg(s->device);
+    std::vector<uint32_t> est(nk), srt(nk);
+    HIPCHECK(hipMemcpyAsync(est.data(), g.est.p, 4 * nk, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipMemcpyAsync(srt.data(), g.est_sorted.p, 4 * nk, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    auto balance = [&](const std::vector<uint32_t>& v, bool inv) {
+      double smax = 0, smean = 0;
+      for (uint64_t w = 0; w < nk; w += 64) {
+        const uint64_t e = std::min<uint64_t>(w + 64, nk);
+        double mx = 0, sum = 0;
+        for (uint64_t i = w; i < e; i++) {
+          const double x = (double)(inv ? ~v[i] : v[i]);  // the sort keeps ~est (descending)
+          mx = std::max(mx, x);
+          sum += x;
+        }
+        smax += mx;
+        smean += sum / (double)(e - w);
+      }
+      return smean > 0 ? smax / smean : 1.0;
+    };
+    *ordered = balance(srt, true);
+    *identity = balance(est, false);
   });
 }
 

@@ -27,7 +27,7 @@ EXPORTS = [
     "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
     "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
     "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
-    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals", "cep_symbol_keys",
+    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals", "cep_symbol_keys", "cep_lane_balance",
 ]
 
 
@@ -113,6 +113,7 @@ def lib():
             "cep_decode_stock_json": ([C.c_int, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
             "cep_synth_stock_json": ([C.c_int, vp, vp, u64, vp, u64, vp, C.POINTER(u64)], C.c_int),
             "cep_symbol_keys": ([C.c_int, vp, vp, vp, vp, u64, u64, vp, C.POINTER(u64), vp], C.c_int),
+            "cep_lane_balance": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -515,6 +516,13 @@ class Session:
         ms, aux, n = C.c_double(), C.c_double(), C.c_uint64()
         _check(lib().cep_timing_totals(self.h, query, 1 if reset else 0, C.byref(ms), C.byref(aux), C.byref(n)))
         return ms.value, aux.value, n.value
+
+    def lane_balance(self, query: int = 0):
+        """cep_lane_balance: (longest-first lane order, key-index order) sum-over-waves of the
+        busiest lane's work estimate / the mean lane's (1.0 = no lane idles)."""
+        o, i = C.c_double(), C.c_double()
+        _check(lib().cep_lane_balance(self.h, query, C.byref(o), C.byref(i)))
+        return o.value, i.value
 
     def stats(self, query: int = 0) -> dict:
         """cep_last_stats: the last batch's NFA figures for the query's kernel group."""

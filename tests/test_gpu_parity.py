@@ -494,3 +494,18 @@ def test_arrival_rejects_bad_key():
     s = N.Session(N.Query(W.stock_query("readme").to_ir()))
     with pytest.raises(N.CepError):
         s.push_arrival(np.array([0, 5], np.uint32), [np.array([1, 2], np.int32), np.array([1, 2], np.int32)], 2)
+
+
+def test_lane_balance_figure():
+    """cep_lane_balance: the longest-first lane order packs waves of similar work (closer to
+    1.0 than key-index order); both are >= 1 by construction."""
+    cfg = W.SynthConfig("t", "stock", 20000, 300, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    s = N.Session(N.Query(W.stock_query("readme").to_ir()))
+    s.push(off, cols)
+    ordered, identity = s.lane_balance(0)
+    assert 1.0 <= ordered <= identity
+    s2 = N.Session(N.Query(W.strict_abc_query().to_ir()))  # stencil: no lane order
+    s2.push(*W.generate(W.SynthConfig("t", "abc", 100, 100, 1)))
+    with pytest.raises(N.CepError):
+        s2.lane_balance(0)
