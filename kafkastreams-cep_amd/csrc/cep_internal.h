@@ -72,7 +72,7 @@ hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, cons
                          const uint32_t* m_emit, const uint64_t* m_off, const uint32_t* p_seq,
                          const uint16_t* p_stage, unsigned long long* out, hipStream_t st);
 hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
-                            hipStream_t st);
+                            uint32_t* zero, uint32_t n_zero, hipStream_t st);
 uint64_t stencil_waves(uint64_t n_events);
 hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
 uint64_t stencil_tiles(uint64_t n_events);

@@ -45,10 +45,13 @@ constexpr int kWkInline = 16;  // wave starts a thread writes itself; longer key
 // wave_key[w] = the key holding event w * kStWave (wave starts inside key k: ceil(s/W) ..
 // ceil(e/W) - 1; empty keys hold none).  A thread per key; a key spanning more than kWkInline
 // wave starts is written by its whole block (a single key of the whole stream stays parallel).
+// (It also zeroes the batch's counters, `zero[0..n_zero)`, which the mask pass accumulates
+// into after it: one launch fewer per batch than a separate memset.)
 __global__ void __launch_bounds__(256) wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_waves,
-                                                 uint32_t* wave_key) {
+                                                 uint32_t* wave_key, uint32_t* zero, uint32_t n_zero) {
   __shared__ uint32_t s_big[256];
   __shared__ uint32_t s_nbig;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_zero; i += (uint64_t)gridDim.x * 256) zero[i] = 0;
   if (threadIdx.x == 0) s_nbig = 0;
   __syncthreads();
   const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -462,7 +465,10 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
     if (w < wv) woff += s_wsum[w];
   const uint32_t excl = woff + incl - cnt;
   const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
-  if (t + 1 == gridDim.x && tid == kStThreads - 1) *A.total = toff + woff + incl;  // all matches
+  if (t + 1 == gridDim.x && tid == kStThreads - 1) {  // all matches
+    *A.total = toff + woff + incl;
+    if (A.total_host) *A.total_host = toff + woff + incl;  // pinned host memory, read after the batch's event
+  }
   const uint32_t tile_total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
   const bool staged = tile_total <= kStage;  // block-uniform
   uint64_t o = toff + excl;
@@ -512,11 +518,11 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
 
 // ---------------------------------------------------------------- host launchers
 hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
-                            hipStream_t st) {
+                            uint32_t* zero, uint32_t n_zero, hipStream_t st) {
   const uint64_t n_waves = (n_events + kStWave - 1) / kStWave;
-  if (n_keys == 0 || n_waves == 0) return hipSuccess;
+  if (n_keys == 0 || n_waves == 0) return hipMemsetAsync(zero, 0, 4ull * n_zero, st);
   hipLaunchKernelGGL(wave_keys, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, n_waves,
-                     wave_key);
+                     wave_key, zero, n_zero);
   return hipGetLastError();
 }
 

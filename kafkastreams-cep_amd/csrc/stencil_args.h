@@ -32,6 +32,7 @@ struct StencilArgs {
   uint32_t* m_key;
   uint32_t* p_seq;           // [n_matches * m]
   uint64_t* total;           // number of matches (written by the last tile of stencil_emit)
+  uint64_t* total_host;      // the same, into the session's pinned host copy (no D2H copy per batch)
   uint64_t out_cap;          // matches that fit the output arrays
   uint32_t* overflow;
 };
