@@ -813,13 +813,20 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "    if (" + predName[d.begin_stage][0] + "(e, f, err, K) || err) return true;\n  }\n  return false;\n}\n";
     // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
     // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
-    // One wave per key: the key's events are contiguous, so its loads coalesce.
+    // One wave per key, read from the begin-hit bitmap (launched first): a lane per 64-event
+    // word, 1 bit per event instead of the predicate's columns.
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_est(NfaArgs A) {\n";
     o += "  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n  const uint32_t lane = threadIdx.x & 63;\n";
     o += "  if (k >= A.n_keys) return;\n";
     o += "  const uint64_t base = A.key_off[k];\n  const uint32_t n = (uint32_t)(A.key_off[k + 1] - base);\n";
-    o += "  uint64_t w = 0;\n  for (uint32_t j = lane; j < n; j += 64)\n";
-    o += "    if (begin_hit_at(A, base + j)) w += n - j;\n";
+    o += "  uint64_t w = 0;\n";
+    o += "  const uint64_t p1 = base + n;\n";
+    o += "  for (uint64_t wi = (base >> 6) + lane; n > 0 && wi <= ((p1 - 1) >> 6); wi += 64) {\n";
+    o += "    uint64_t bits = A.bhits[wi];\n    const uint64_t s = wi << 6;\n";
+    o += "    if (s < base) bits &= ~0ull << (base - s);\n";
+    o += "    if (p1 - s < 64) bits &= (1ull << (p1 - s)) - 1ull;\n";
+    o += "    while (bits) {\n      const uint32_t b = (uint32_t)__builtin_ctzll(bits);\n      bits &= bits - 1ull;\n";
+    o += "      w += n - (uint32_t)(s + b - base);\n    }\n  }\n";
     o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";

@@ -480,7 +480,12 @@ void run_nfa(cep_session* s, GroupRt& g) {
   float total_ms = 0;
   uint32_t launches = 0;
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
-  // Lane order: keys sorted by estimated work, longest first (cep_nfa_est), so a wave's 64
+  if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
+    s->bhits.ensure(8 * ((s->n_events + 63) / 64));
+    a.bhits = s->bhits.as<uint64_t>();
+    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 255) / 256, s->stream));
+  }
+  // Lane order: keys sorted by estimated work, longest first (cep_nfa_est, from the begin-hit bitmap), so a wave's 64
   // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
   // start first.  Streams keep the identity order (their run queues live at the key's slot).
   if (g.fn_est && !streaming && nk > 64) {
@@ -496,11 +501,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
     g.est_valid = true;
   } else {
     g.est_valid = false;
-  }
-  if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
-    s->bhits.ensure(8 * ((s->n_events + 63) / 64));
-    a.bhits = s->bhits.as<uint64_t>();
-    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 255) / 256, s->stream));
   }
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
   HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream));
