@@ -362,7 +362,10 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // Per-batch sessions run persistent lanes (nfa_lane.h run_jobs): a grid of about what the
   // chip holds at once (3 waves per SIMD), every lane claiming job after job.  Streams keep one
   // lane per key (their run queues live at the key's slot).
-  const uint64_t resident = (uint64_t)s->cus * 12 * 64;
+  uint64_t waves_cu = 12;  // 3 per SIMD (the JIT kernel's occupancy); $CEP_RESIDENT_WAVES (per CU): measurement runs
+  if (const char* e = std::getenv("CEP_RESIDENT_WAVES"))
+    if (std::atoi(e) > 0) waves_cu = (uint64_t)std::atoi(e);
+  const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
   auto grid_for = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident); };
   // $CEP_NO_PERSIST / $CEP_PERSIST (measurement runs): one lane per job / persistent lanes
   // (single queries run one lane per key: their longest-first lane order already balances the
