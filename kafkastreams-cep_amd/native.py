@@ -462,9 +462,17 @@ class Session:
         return ko, ai, ms.value
 
     def push_device(self, stream: DeviceStream, ts_ptr=None):
-        ptrs = (C.c_void_p * len(stream.cols))(*[c.ptr for c in stream.cols])
-        b = Batch(stream.n_keys, stream.n_events, stream.key_off.ptr, ptrs, ts_ptr, CEP_MEM_DEVICE)
-        _check(lib().cep_push_batch(self.h, C.byref(b)))
+        # the batch descriptor of a device-resident stream is built once and reused (pushing the
+        # same buffers again is the bench's steady state; a stencil push is ~0.1 ms of GPU work,
+        # so host-side microseconds per call show up between batches)
+        key = (id(stream), ts_ptr)
+        cached = getattr(self, "_dev_batch", None)
+        if cached is None or cached[0] != key or cached[1] is not stream:
+            ptrs = (C.c_void_p * len(stream.cols))(*[c.ptr for c in stream.cols])
+            b = Batch(stream.n_keys, stream.n_events, stream.key_off.ptr, ptrs, ts_ptr, CEP_MEM_DEVICE)
+            cached = (key, stream, ptrs, b, C.byref(b))
+            self._dev_batch = cached
+        _check(lib().cep_push_batch(self.h, cached[4]))
         self.n_keys = stream.n_keys
 
     # -- output --
