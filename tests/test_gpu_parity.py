@@ -324,6 +324,21 @@ def test_watermark():
     off = np.array([0, 3], np.uint64)
     s.push(off, [np.array([1, 2, 3], np.int32), np.array([1, 2, 3], np.int32)], ts=np.array([5, 9, 7]))
     assert s.watermark() == 9
+    # the max kernel's 16-byte path, its odd tail and a lone event; the maximum first, inside, last
+    rng = np.random.default_rng(11)
+    for n in (1, 2, 5, 1001, (1 << 20) + 3):
+        for where in (0, n // 2, n - 1):
+            ts = rng.integers(-(1 << 40), 1 << 40, n)
+            ts[where] = (1 << 41) + n
+            off = np.array([0, n], np.uint64)
+            s.push(off, [np.zeros(n, np.int32), np.zeros(n, np.int32)], ts=ts)
+            assert s.watermark() == (1 << 41) + n
+    # an 8-byte-aligned device pointer (the scalar path)
+    d = N.synth_stream("stock", 5, 40, 30)
+    t = N.synth_ts(d.n_events + 1, -7)
+    s2 = N.Session(q)
+    s2.push_device(d, t.ptr + 8)
+    assert s2.watermark() == -7 + d.n_events
 
 
 def test_cfg2_full_size_checksum():
