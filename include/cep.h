@@ -222,7 +222,8 @@ int cep_watermark(cep_session* s, int64_t* out);
 /* Device time of the last batch, per query, from HIP events recorded on the session
  * stream (ms): the matching kernel launches (kernel_ms, `launches` of them: the NFA kernel
  * incl. capacity retries, or stencil_mask + stencil_emit) and the
- * setup/compaction kernels (aux_ms). */
+ * setup/compaction kernels (aux_ms; 0 for a stencil batch, whose 4 us key-index pass is left
+ * unbracketed: an event marker costs the stream about as much). */
 /* ---- streaming-session snapshot / restore ----
  * The reference's persistent mode stores the NFA's run queue and buffer nodes after every
  * record (CEPProcessor.java:121-131,159-160; nfa/ComputationStageSerDe.java:53-125;

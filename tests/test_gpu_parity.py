@@ -125,7 +125,7 @@ def test_stencil_pipelined_pushes():
     for off, cols in batches:
         s.push(off, cols)
     ms, aux, n = s.timing_totals(0)
-    assert n == 20 and ms > 0 and aux > 0
+    assert n == 20 and ms > 0 and aux == 0  # (the stencil's key-index pass is not timed)
     off, cols = batches[-1]
     assert_parity(session_result(s, 0, off, q.kind), oracle.run(q.ir, off, cols), off)
     s.timing_totals(0, reset=True)
