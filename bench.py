@@ -258,6 +258,7 @@ def cfg4(device, stream, steps, warmup, dist, threads, cpu_every):
     res = {"workload": f"cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms, {stream.n_keys} keys x ~1000 "
                        f"events ({stream.n_events} events) on 1 GPU",
            "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
+           "steps": steps, "warmup": warmup,
            "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
            "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
            "buffer_preds_per_key": st["preds_used"] / max(1, stream.n_keys),
@@ -285,6 +286,7 @@ def semantic_cfg4(device, stream, ts, steps, warmup, dist, threads, cpu_every):
     res = {"workload": f"cfg4 query, semantic WITHIN 10 ms (runs expire), {stream.n_keys} keys x ~1000 events "
                        f"({stream.n_events} events), ts = 1.6e12 + position",
            "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
+           "steps": steps, "warmup": warmup,
            "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
            "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
            "roofline": roofline(alg, kms, "cep_nfa_jit", "cep_nfa_jit_semantic")}
@@ -540,10 +542,12 @@ def main():
                                                gpu_digests([W.stock_query(args.variant)], device))
         if one and not args.no_other:
             log("cfg4")
-            ok = max(1, args.steps // 5)
-            out["other_configs"] = {"cfg4": cfg4(device, stream, ok, 1, dist, args.cpu_threads, 64 if cpu else 0)}
+            # (a config-4 step is 5-10 ms: 10 timed steps after 3 warmup ones, the first of
+            # which size the session's pools)
+            ok, ow = max(10, args.steps), max(3, args.warmup)
+            out["other_configs"] = {"cfg4": cfg4(device, stream, ok, ow, dist, args.cpu_threads, 64 if cpu else 0)}
             log("cfg4 semantic WITHIN")
-            out["other_configs"]["cfg4_semantic"] = semantic_cfg4(device, stream, ts, ok, 1, dist, args.cpu_threads,
+            out["other_configs"]["cfg4_semantic"] = semantic_cfg4(device, stream, ts, ok, ow, dist, args.cpu_threads,
                                                                    64 if cpu else 0)
         sess.close()
         del stream, ts

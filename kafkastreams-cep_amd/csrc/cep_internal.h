@@ -11,6 +11,9 @@
 #include "cep_layout.h"
 
 namespace cep {
+
+// 256-position strips per workgroup of the begin-hit bitmap kernel (compile.cpp cep_nfa_bits)
+constexpr int kBitStrips = 16;
 struct ParsedQuery;
 }
 

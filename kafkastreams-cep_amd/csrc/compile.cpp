@@ -832,13 +832,15 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
     // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
     // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).
-    // Four 256-position strips per block, their loads issued together (one position per
-    // thread per strip keeps every load instruction coalesced).
+    // kBitStrips 256-position strips per block, their loads issued together (one position
+    // per thread per strip keeps every load instruction coalesced; few, longer workgroups:
+    // with 4 strips a 1e9-event batch was 1M workgroups of four loads each, 1.33 ms).
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_bits(NfaArgs A) {\n";
-    o += "  const uint64_t p0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;\n";
-    o += "  bool h[4];\n#pragma unroll\n  for (int k = 0; k < 4; k++) {\n";
+    o += "  constexpr int S = " + std::to_string(kBitStrips) + ";\n";
+    o += "  const uint64_t p0 = (uint64_t)blockIdx.x * (256 * S) + threadIdx.x;\n";
+    o += "  bool h[S];\n#pragma unroll\n  for (int k = 0; k < S; k++) {\n";
     o += "    const uint64_t p = p0 + (uint64_t)k * 256;\n    h[k] = p < A.n_events && begin_hit_at(A, p);\n  }\n";
-    o += "#pragma unroll\n  for (int k = 0; k < 4; k++) {\n    const uint64_t p = p0 + (uint64_t)k * 256;\n";
+    o += "#pragma unroll\n  for (int k = 0; k < S; k++) {\n    const uint64_t p = p0 + (uint64_t)k * 256;\n";
     o += "    const uint64_t b = __ballot(h[k]);\n";
     o += "    if ((threadIdx.x & 63) == 0 && p < A.n_events) A.bhits[p >> 6] = b;\n  }\n}\n\n";
   }

@@ -486,7 +486,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
     s->bhits.ensure(8 * ((s->n_events + 63) / 64));
     a.bhits = s->bhits.as<uint64_t>();
-    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 1023) / 1024, s->stream));  // 1024 positions per block
+    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 256 * kBitStrips - 1) / (256 * kBitStrips), s->stream));
   }
   // Lane order: keys sorted by estimated work, longest first (cep_nfa_est, from the begin-hit bitmap), so a wave's 64
   // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
