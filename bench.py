@@ -45,6 +45,21 @@ TS_BASE = 1_600_000_000_000  # ts = 1.6e12 + position (ms)
 _T0 = time.time()
 
 
+def cpu_share():
+    """(host threads for the CPU baseline, nproc): the cgroup CPU quota when one is set (a
+    GPU box's share of the machine), else every CPU this process may run on.  os.cpu_count()
+    is reported beside it as `nproc`."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n), os.cpu_count() or 1
+
+
 def log(msg):
     """progress on stderr (the JSON line alone goes to stdout)"""
     print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
@@ -188,7 +203,7 @@ def cpu_baseline(cfg, queries, threads, every, gpu_check=None, extrapolated=Fals
         want.append((r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]),
                      int(np.count_nonzero(r["err_code"]))))
     out = {"value": n_ev * len(queries) / el, "unit": "events/s" if len(queries) == 1 else "query-events/s",
-           "cores": r["threads"], "kind": "port",
+           "cores": r["threads"], "nproc": cpu_share()[1], "kind": "port",
            "sample": f"{len(keys)} of {cfg.n_keys} keys (every {every}th), {n_ev} events x {len(queries)} "
                      f"quer{'y' if len(queries) == 1 else 'ies'}, {n_m} matches, {el:.2f} s on {r['threads']} threads"
                      + (" (rate extrapolated to the full key set)" if extrapolated else ""),
@@ -239,34 +254,42 @@ def secondary_strict(device, steps, warmup, dist, threads, cpu):
         pseq = r["pair_pos"].astype(np.uint64) - off[pk]
         want = W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"])
         res["cpu_baseline"] = {"value": n_ev / r["elapsed_s"], "unit": "events/s", "cores": r["threads"],
-                               "kind": "port", "sample": f"the whole stream ({n_ev} events, {r['n_matches']} matches), "
+                               "nproc": cpu_share()[1], "kind": "port", "sample": f"the whole stream ({n_ev} events, {r['n_matches']} matches), "
                                                          f"{r['elapsed_s']:.2f} s on {r['threads']} threads",
                                "parity_on_sample": bool((r["n_matches"], want) == (n_m, dig))}
     return res
 
 
-def cfg4(device, stream, steps, warmup, dist, threads, cpu_every):
+def cfg4(device, stream, steps, warmup, dist, threads, cpu_every, stress=True):
     """Config 4: skip_till_any Kleene+ with folds and a 10 ms WITHIN over the cfg-3 stream (1M
-    keys): run-explosion / versioned-buffer stress.  Reports buffer nodes per key."""
-    q = N.Query(W.any_kleene_query().to_ir())
+    keys): run-explosion / versioned-buffer stress.  Reports buffer nodes per key.
+    stress=True (the benched figure): workloads.any_kleene_query(carry_volume=True), the variant
+    in which no key throws (SURVEY §8d row 4: "no Appendix-C exception path fires");
+    stress=False: the query as written, the parity case, which throws NPE on about half of
+    the keys in the reference itself (NFA.java:243, ValueStore.java:92-97)."""
+    p = W.any_kleene_query(carry_volume=stress)
+    q = N.Query(p.to_ir())
     s = N.Session(q, device=device)
     el, kms, _ = run_steps(s, stream, steps, warmup, dist)
     n_m, n_pairs, n_err = match_figures(s, 0, stream.n_keys)
     st = s.stats(0)
     s.close()
     alg = 8.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m
-    res = {"workload": f"cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms, {stream.n_keys} keys x ~1000 "
-                       f"events ({stream.n_events} events) on 1 GPU",
+    what = ("S1 also folds volume, S2 reads it with getOrElse: no key throws" if stress else
+            "the query as written (parity case; NPE in the reference on the keys counted in key_errors)")
+    res = {"workload": f"cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms, {what}; {stream.n_keys} keys x "
+                       f"~1000 events ({stream.n_events} events) on 1 GPU",
            "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
            "steps": steps, "warmup": warmup,
            "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
            "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
            "buffer_preds_per_key": st["preds_used"] / max(1, stream.n_keys),
-           "retried_jobs": st["retried_jobs"], "roofline": roofline(alg, kms, "cep_nfa_jit", "cep_nfa_jit_cfg4")}
+           "retried_jobs": st["retried_jobs"],
+           "roofline": roofline(alg, st["main_ms"], "cep_nfa_jit", "cep_nfa_jit_cfg4" + ("s" if stress else ""),
+                                step_kernels_ms=kms)}
     if cpu_every:
         cfg = W.SynthConfig("cfg4", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
-        res["cpu_baseline"] = cpu_baseline(cfg, [W.any_kleene_query()], threads, cpu_every,
-                                           gpu_digests([W.any_kleene_query()], device), extrapolated=True)
+        res["cpu_baseline"] = cpu_baseline(cfg, [p], threads, cpu_every, gpu_digests([p], device), extrapolated=True)
     return res
 
 
@@ -282,6 +305,9 @@ def semantic_cfg4(device, stream, ts, steps, warmup, dist, threads, cpu_every):
     n_m, n_pairs, n_err = match_figures(s, 0, stream.n_keys)
     st = s.stats(0)
     s.close()
+    # priced at step level: the step streams price + volume (begin-hit bitmap) and the
+    # timestamps (watermark, expiry) once, but cep_nfa_jit itself skips most of those bytes
+    # (quiet lanes jump 64 events per bitmap word), so a kernel-level price would overstate it
     alg = 16.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m  # price, volume, ts
     res = {"workload": f"cfg4 query, semantic WITHIN 10 ms (runs expire), {stream.n_keys} keys x ~1000 events "
                        f"({stream.n_events} events), ts = 1.6e12 + position",
@@ -289,11 +315,99 @@ def semantic_cfg4(device, stream, ts, steps, warmup, dist, threads, cpu_every):
            "steps": steps, "warmup": warmup,
            "matches_per_step": n_m, "pairs_per_step": n_pairs, "key_errors": n_err,
            "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
-           "roofline": roofline(alg, kms, "cep_nfa_jit", "cep_nfa_jit_semantic")}
+           "roofline": roofline(alg, 1e3 * el / steps, "whole step (cep_nfa_bits, cep_nfa_est, lane order, "
+                                "watermark max, cep_nfa_jit, compaction)", "cfg4_semantic_step",
+                                cep_nfa_jit_ms=st["main_ms"], step_kernels_ms=kms)}
     if cpu_every:
         cfg = W.SynthConfig("cfg4s", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
         res["cpu_baseline"] = cpu_baseline(cfg, [p], threads, cpu_every, gpu_digests([p], device, True),
                                            extrapolated=True, semantic=True)
+    return res
+
+
+def slice_stream(stream, slices):
+    """The stream cut into `slices` consecutive batches per key: batch b holds key k's events
+    j with n_k*b/slices <= j < n_k*(b+1)/slices (gathered on the device)."""
+    off = stream.key_off.download(np.uint64, stream.n_keys + 1).astype(np.int64)
+    n = np.diff(off)
+    parts = []
+    for b in range(slices):
+        lo, hi = n * b // slices, n * (b + 1) // slices
+        parts.append(N.gather_ranges(stream, (off[:-1] + lo).astype(np.uint64), (off[:-1] + hi).astype(np.uint64)))
+    return parts
+
+
+def streaming_cfg3(device, stream, slices, steps, dist, warmup=1, variant="readme"):
+    """The path CEPProcessor uses (processor.py): a streaming session, each key's NFA carried
+    from batch to batch (cep_opts.streaming; NFA.java:94-109 driven per record by
+    CEPProcessor.java:155-163).  The cfg-3 stream is pushed as `slices` consecutive batches
+    (about 1000/slices events per key each); a step = all of them, every key starting from the
+    NFA's initial state.  Exactness at full size: the sum of the batches'
+    checksums equals the per-batch session's checksum of the whole stream (the same matches
+    with the same per-key sequence numbers), checked on one untimed pass."""
+    parts = slice_stream(stream, slices)
+    q = N.Query(W.stock_query(variant).to_ir())
+    times, kern = [], []
+    s = N.Session(q, device=device, streaming=True)
+    for it in range(warmup + steps):
+        s.reset()  # every key back to the initial state (the warmup sized the pools)
+        dist.barrier()
+        t0 = time.perf_counter()
+        km = 0.0
+        for p in parts:
+            s.push_device(p)
+            km += s.stats(0)["kernel_ms"]
+        N.lib().cep_sync(s.h)
+        el = time.perf_counter() - t0
+        if it >= warmup:
+            times.append(el)
+            kern.append(km)
+    # the untimed verification pass: matches, errors and checksums summed over the batches
+    s.reset()
+    n_m = n_p = 0
+    dig = 0
+    for p in parts:
+        s.push_device(p)
+        m, d = s.digest(0)
+        _, pairs, _ = match_figures(s, 0, p.n_keys)
+        n_m += m
+        n_p += pairs
+        dig = (dig + d) % (1 << 64)
+    code, _ = s.key_errors(0, stream.n_keys)
+    s.close()
+    el = float(np.mean(times))
+    return {"workload": f"cfg3 README stock query as {slices} consecutive batches of a streaming session "
+                        f"({stream.n_keys} keys, ~{stream.n_events // max(1, stream.n_keys * slices)} events per key "
+                        f"per batch, {stream.n_events} events per step)",
+            "value": stream.n_events / el, "unit": "events/s", "ms_per_step": 1e3 * el, "steps": steps,
+            "warmup": warmup, "kernel_ms_per_step": float(np.mean(kern)), "matches_per_step": n_m,
+            "pairs_per_step": n_p, "key_errors": int(np.count_nonzero(code)), "checksum": f"{dig:016x}"}
+
+
+def projected_scaling(device, cfg, stream, world, steps, dist, t1_ms=None):
+    """SURVEY §8(e) strong scaling, projected on ONE GPU: every rank's murmur2 shard of the
+    cfg-3 stream (shard.py, the same split bench.py makes at --gpus N) is run alone, one after
+    the other; the projected N-GPU step is the slowest rank's, and the projected efficiency
+    t1 / (N x that).  A projection, not a measured multi-GPU curve (no collective, no
+    contention between GPUs)."""
+    off = stream.key_off.download(np.uint64, stream.n_keys + 1)
+    q = N.Query(W.stock_query("readme").to_ir())
+    per = []
+    for r in range(world):
+        keys, loff = SH.shard_layout(off, world, r)
+        sh, _ = N.shard_stream(stream, keys, loff)
+        s = N.Session(q, device=device)
+        el, kms, _ = run_steps(s, sh, steps, 1, dist)
+        per.append({"rank": r, "keys": int(len(keys)), "events": int(sh.n_events), "ms_per_step": 1e3 * el / steps,
+                    "kernel_ms": s.stats(0)["main_ms"]})
+        s.close()
+        del sh
+    worst = max(p["ms_per_step"] for p in per)
+    res = {"world": world, "per_rank": per, "projected_ms_per_step": worst,
+           "note": "projection: each rank's shard run alone on one GPU, not a measured multi-GPU curve"}
+    if t1_ms:
+        res["t1_ms_per_step"] = t1_ms
+        res["projected_efficiency"] = t1_ms / (world * worst)
     return res
 
 
@@ -451,13 +565,15 @@ def main():
     ap.add_argument("--mean", type=int, default=1000, help="mean events per key")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--variant", default="readme", choices=["readme", "test"])
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=cpu_share()[0])
     ap.add_argument("--cpu-every", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the arrival-order end-to-end figure")
     ap.add_argument("--no-other", action="store_true", help="skip the cfg 4 / cfg 5 figures")
     ap.add_argument("--no-ingest", action="store_true", help="skip the JSON ingest figure")
+    ap.add_argument("--no-projection", action="store_true", help="skip the projected 8-GPU strong scaling")
+    ap.add_argument("--no-streaming", action="store_true", help="skip the streaming-session figure")
     ap.add_argument("--ingest-keys", type=int, default=100_000, help="keys of the JSON ingest figure")
     ap.add_argument("--cfg5-keys", type=int, default=1_000_000)
     ap.add_argument("--cfg5-batch", type=int, default=125_000, help="keys per pushed batch of config 5")
@@ -540,12 +656,22 @@ def main():
             log("cfg3 cpu baseline")
             out["cpu_baseline"] = cpu_baseline(cfg, [W.stock_query(args.variant)], args.cpu_threads, args.cpu_every,
                                                gpu_digests([W.stock_query(args.variant)], device))
+        if one and not args.no_projection:
+            log("projected strong scaling")
+            out["projected_scaling"] = projected_scaling(device, cfg, stream, 8, args.steps, dist,
+                                                         t1_ms=out["ms_per_step"])
+        if one and not args.no_streaming:
+            log("streaming")
+            out["streaming"] = streaming_cfg3(device, stream, 10, max(1, min(args.steps, 5)), dist)
         if one and not args.no_other:
             log("cfg4")
             # (a config-4 step is 5-10 ms: 10 timed steps after 3 warmup ones, the first of
             # which size the session's pools)
             ok, ow = max(10, args.steps), max(3, args.warmup)
             out["other_configs"] = {"cfg4": cfg4(device, stream, ok, ow, dist, args.cpu_threads, 64 if cpu else 0)}
+            log("cfg4 as written")
+            out["other_configs"]["cfg4_literal"] = cfg4(device, stream, ok, ow, dist, args.cpu_threads,
+                                                        64 if cpu else 0, stress=False)
             log("cfg4 semantic WITHIN")
             out["other_configs"]["cfg4_semantic"] = semantic_cfg4(device, stream, ts, ok, ow, dist, args.cpu_threads,
                                                                    64 if cpu else 0)

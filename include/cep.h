@@ -151,7 +151,7 @@ void cep_session_destroy(cep_session* s);
 /* A key-partitioned (CSR) column batch: events of key k are positions
  * key_off[k] .. key_off[k+1]-1, in arrival order.  cols[f] holds n_events values of the
  * IR field type f.  ts may be NULL (timestamps are not read by WITHIN in the reference:
- * its windows never prune).  Buffers are borrowed for the call only. */
+ * its windows never prune).  Buffer lifetime: see cep_push_batch. */
 typedef struct {
   uint64_t n_keys;
   uint64_t n_events;
@@ -172,9 +172,21 @@ typedef struct {
  * batch starts every key from the NFA's initial state.  A streaming session cannot re-run a
  * key: one that hits a limit (CEP_KEY_CAPACITY: size max_runs for the query) stops there,
  * like a key whose query threw; its buffer walks run in place (no CEP_KEY_CONFLICT), and
- * stencil-kind queries run on the NFA kernel.  Returns once the batch's kernels have
- * completed (buffers are borrowed for the call only). */
+ * stencil-kind queries run on the NFA kernel.
+ * Buffer lifetime.  CEP_MEM_HOST batches are copied to the device before the call returns:
+ * their buffers are borrowed for the call only.  CEP_MEM_DEVICE batches are read in place:
+ * NFA batches finish before the call returns, but stencil-kind queries and the watermark
+ * run asynchronously on the session stream, so a device batch stays borrowed until the next
+ * result call on the session (cep_poll_matches, cep_match_digest, cep_key_errors,
+ * cep_watermark, cep_last_timing/stats, cep_timing_totals), the next push, cep_sync or
+ * cep_session_destroy returns. */
 int cep_push_batch(cep_session* s, const cep_batch* b);
+
+/* Streaming sessions: every key back to the NFA's initial state (NFA.initComputationStates,
+ * nfa/NFA.java:74-81) - run queues, buffer nodes and sequence numbers dropped, device
+ * allocations kept for the next stream.  A no-op for per-batch sessions (every batch starts
+ * fresh there). */
+int cep_session_reset(cep_session* s);
 
 /* Layout of the last batch as the matchers saw it: key_off [n_keys + 1] and, for an
  * arrival-order batch, arrival_index [n_events] (the arrival position of each CSR position;
@@ -324,26 +336,6 @@ int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_
 int cep_symbol_keys(int device, const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* name_span,
                     const int32_t* status, uint64_t n_records, uint64_t max_symbols, uint32_t* key_out,
                     uint64_t* n_symbols, void* stream);
-
-/* ---- synthetic workloads (bench / tests): kafkastreams-cep_amd/workloads.py, on device ----
- * kind 0 = "abc" (one int column v = h % 16), 1 = "stock" (int price random walk, int volume).
- * Fills device buffers: key_off [n_keys+1] (u64), cols[0..] (int32, n_events each).
- * cep_synth_count returns n_events for sizing. */
-int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
-                    uint32_t mean_events, uint64_t* n_events);
-/* Timestamps of a synthetic CSR stream in device memory: ts[i] = base + i (CSR position). */
-int cep_synth_ts(int device, uint64_t n_events, int64_t base, int64_t* ts_dev);
-int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
-                       uint32_t mean_events, uint64_t* key_off_dev, int32_t* const* cols_dev);
-/* The same stream in arrival order (round robin: ordered by (index within key, key)): the key
- * of every event in keys_dev [n_events], values in cols_dev. */
-int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
-                               uint32_t mean_events, uint32_t* keys_dev, int32_t* const* cols_dev);
-/* StockEvent JSON values of n events as json-simple serializes them (StockEventSerDe.java:75-82),
- * {"name":"e<i+1>","price":P,"volume":V} (README.md:73-80): rec_off_dev[n+1] and *total (bytes)
- * are always written; the text goes to out_dev only when *total <= cap. */
-int cep_synth_stock_json(int device, const int32_t* price_dev, const int32_t* volume_dev, uint64_t n,
-                         uint8_t* out_dev, uint64_t cap, uint64_t* rec_off_dev, uint64_t* total);
 
 #ifdef __cplusplus
 }

@@ -82,13 +82,7 @@ uint64_t stencil_tiles(uint64_t n_events);
 hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
                                     void* price, void* volume, int32_t* status, uint32_t* name_span,
                                     hipStream_t st);
-hipError_t synth_stock_json(const int32_t* price, const int32_t* volume, uint64_t n, uint8_t* out, uint64_t cap,
-                            uint64_t* rec_off, uint64_t* total);
-hipError_t launch_synth(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, const uint64_t* key_off,
-                        int32_t* c0, int32_t* c1, hipStream_t st);
-hipError_t launch_synth_ts(int64_t* ts, uint64_t n, int64_t base, hipStream_t st);
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
-uint64_t synth_hash_host(uint64_t seed, uint64_t key, uint64_t j);
 std::vector<char> jit_code_object(const std::string& src, double* compile_s);
 struct Cols;
 size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
@@ -99,8 +93,6 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
 // keys 0..n-1 ordered by est descending -> order (tmp: scratch grown as needed)
 hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st);
-hipError_t csr_to_arrival(const uint64_t* key_off, uint64_t n_keys, uint64_t n, uint64_t max_nk, const int32_t* c0,
-                          const int32_t* c1, uint32_t* key_out, int32_t* o0, int32_t* o1, hipStream_t st);
 std::string jit_cache_key(const std::string& src);
 hipError_t gather_keys(uint64_t n_sel, const uint32_t* sel, const uint64_t* src_off, const uint64_t* dst_off,
                        int nf, const uint32_t* col_bytes, const void* const* src_cols, void* const* dst_cols,

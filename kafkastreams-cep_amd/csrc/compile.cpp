@@ -534,7 +534,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
   o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
   // tuning knobs of nfa_lane.h, for measurement runs only ($CEP_WALK_FLUSH, $CEP_QUIET_CHUNK)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN"})
+  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   if (lits.param) o += "#define CEP_WALK_COMPAT2 1  // kernel group: the wider straight-line walk step\n";

@@ -30,7 +30,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include "json_parser.h"
 
@@ -133,76 +132,6 @@ hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_of
   hipLaunchKernelGGL(decode_stock_json_general, grid2, dim3(kIngestBlock), 0, st, bytes, rec_off, n, col_width,
                      price, volume, status, name_span);
   return hipGetLastError();
-}
-
-// ---- synthetic records: json-simple's toJSONString of the demo's StockEvent
-// (StockEventSerDe.java:75-82), {"name":"e<i+1>","price":P,"volume":V}, the README's format
-// (README.md:73-80) ----
-
-__device__ __forceinline__ uint32_t ndigits(int64_t v) {
-  uint64_t m = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
-  uint32_t d = 1;
-  while (m >= 10) { m /= 10; d++; }
-  return d + (v < 0);
-}
-
-__global__ void __launch_bounds__(256) json_len_kernel(const int32_t* price, const int32_t* volume, uint64_t n,
-                                                       uint64_t* len) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) len[i] = 31 + ndigits((int64_t)i + 1) + ndigits(price[i]) + ndigits(volume[i]);
-}
-
-__device__ __forceinline__ uint64_t put_str(uint8_t* o, uint64_t p, const char* s) {
-  while (*s) o[p++] = (uint8_t)*s++;
-  return p;
-}
-__device__ __forceinline__ uint64_t put_int(uint8_t* o, uint64_t p, int64_t v) {
-  const uint32_t d = ndigits(v);
-  uint64_t m = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
-  if (v < 0) o[p] = '-';
-  for (uint32_t k = 0; k < d - (v < 0); k++) {
-    o[p + d - 1 - k] = (uint8_t)('0' + m % 10);
-    m /= 10;
-  }
-  return p + d;
-}
-
-__global__ void __launch_bounds__(256) json_write_kernel(const int32_t* price, const int32_t* volume, uint64_t n,
-                                                         const uint64_t* off, uint8_t* out) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  uint64_t p = off[i];
-  // json-simple's JSONObject (a HashMap) iterates volume, price, name (StockEventSerDe.java:75-82)
-  p = put_str(out, p, "{\"volume\":");
-  p = put_int(out, p, volume[i]);
-  p = put_str(out, p, ",\"price\":");
-  p = put_int(out, p, price[i]);
-  p = put_str(out, p, ",\"name\":\"e");
-  p = put_int(out, p, (int64_t)i + 1);
-  p = put_str(out, p, "\"}");
-}
-
-// lengths -> rec_off (inclusive scan into rec_off+1) ; total bytes returned through *total
-hipError_t synth_stock_json(const int32_t* price, const int32_t* volume, uint64_t n, uint8_t* out, uint64_t cap,
-                            uint64_t* rec_off, uint64_t* total) {
-  hipError_t e;
-  if ((e = hipMemset(rec_off, 0, 8)) != hipSuccess) return e;
-  if (n == 0) { *total = 0; return hipSuccess; }
-  const dim3 g((uint32_t)((n + 255) / 256));
-  hipLaunchKernelGGL(json_len_kernel, g, dim3(256), 0, 0, price, volume, n, rec_off + 1);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  size_t tmp = 0;
-  if ((e = hipcub::DeviceScan::InclusiveSum(nullptr, tmp, rec_off + 1, rec_off + 1, (int)n)) != hipSuccess) return e;
-  void* scratch = nullptr;
-  if ((e = hipMalloc(&scratch, tmp + 16)) != hipSuccess) return e;
-  e = hipcub::DeviceScan::InclusiveSum(scratch, tmp, rec_off + 1, rec_off + 1, (int)n);
-  if (e == hipSuccess) e = hipMemcpy(total, rec_off + n, 8, hipMemcpyDeviceToHost);
-  (void)hipFree(scratch);
-  if (e != hipSuccess) return e;
-  if (*total > cap) return hipSuccess;  // caller sees total > cap and retries with more room
-  hipLaunchKernelGGL(json_write_kernel, g, dim3(256), 0, 0, price, volume, n, rec_off, out);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return hipDeviceSynchronize();
 }
 
 }  // namespace cep

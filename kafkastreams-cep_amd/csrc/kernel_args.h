@@ -53,6 +53,7 @@ struct NfaArgs {
                              // throws at CSR position p (quiet lanes jump to the next set bit)
   uint64_t n_events;         // CSR positions of the batch (bits kernel)
   uint32_t* n_capacity_err;  // jobs to re-run (KE_RETRY / KE_CONFLICT)
+  unsigned long long* prof;  // measurement builds ($CEP_PROF): the time split of nfa_lane.h, 16 counters
 };
 
 }  // namespace cep

@@ -75,6 +75,22 @@ extern uint64_t cep_lane_stats[8];  // events, records, walks, walk nodes, pred 
 #define CEP_STAT(i) ((void)0)
 #endif
 
+// Time split of a launch (measurement builds only: $CEP_PROF at query compile, NfaArgs.prof):
+// per wave, shader-clock cycles in each part of the job loop, summed over waves by lane 0.
+//   0 walk drains mid-job   1 quiet skip (bitmap / scan)   2 record loop (steps, lookups, puts)
+//   3 begin run             4 finals + queue swap          5 final drain
+//   6 waves                 7 whole run()                  8 loop iterations   9 records stepped
+//   10 lane-events (event() entered)                        11 walk nodes
+#ifdef CEP_PROF
+#define CEP_PT(v) const uint64_t v = clock64()
+#define CEP_PACC(i, d) (prof[i] += (d))
+#define CEP_LPACC(L, i, d) ((L).prof[i] += (d))
+#else
+#define CEP_PT(v) ((void)0)
+#define CEP_PACC(i, d) ((void)0)
+#define CEP_LPACC(L, i, d) ((void)0)
+#endif
+
 namespace cep {
 
 constexpr uint32_t kNoSk = 0xFF;
@@ -171,6 +187,16 @@ struct Lane {
   uint32_t wq_n = 0;  // queued
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
+#ifdef CEP_PROF
+  unsigned long long prof[12] = {};  // the time split (see CEP_PROF above), this wave / lane
+  // lane 0 adds the wave's cycles, the lane counters summed over the wave
+  __device__ void prof_flush() {
+    for (int i = 9; i < 12; i++)
+      for (int o = 32; o > 0; o >>= 1) prof[i] += __shfl_xor(prof[i], o, 64);
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < 12; i++) atomicAdd(A.prof + i, prof[i]);
+  }
+#endif
 
   __device__ Lane(const NfaArgs& a, Q& qq) : A(a), q(qq) {}
 
@@ -607,6 +633,7 @@ struct Lane {
       return false;
     }
     CEP_STAT(3);
+    CEP_PACC(11, 1);
     Node& n = A.nodes[s];
     WalkPre P;
     walk_load(s, P);
@@ -779,6 +806,8 @@ struct Lane {
   // ---------------------------------------------------------------- one event
   __device__ __forceinline__ void event(bool begin_hit) {
     CEP_STAT(0);
+    CEP_PACC(10, 1);
+    CEP_PT(te0);
     const uint32_t pf = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
     n_final = 0;
@@ -794,11 +823,14 @@ struct Lane {
       load(half, i, c, pf);
       const int produced = q.step(*this, c);
       if (err) return;
+      CEP_PACC(9, 1);
       if (produced == 0) {  // removePattern
         walk_remove(q.stage_sk(c.stage), c.event, c.ev_first, c.ver, false);
         if (err) return;
       }
     }
+    CEP_PT(te1);
+    CEP_PACC(2, te1 - te0);
     // the begin run, last in the queue: its predicate runs after every other record's
     // (an exception from it must not pre-empt theirs)
     if (kBeginReg && !begin_hit) {
@@ -817,6 +849,8 @@ struct Lane {
       q.step(*this, b);
       if (err) return;
     }
+    CEP_PT(te2);
+    CEP_PACC(3, te2 - te1);
     const uint32_t oh = half ^ 1u;
     half = oh;
     count = ocount;
@@ -824,7 +858,11 @@ struct Lane {
       ev = nev;
       ev_pos = j + 1;
     }
-    if (!n_final) return;
+    if (!n_final) {
+      CEP_PT(te3);
+      CEP_PACC(4, te3 - te2);
+      return;
+    }
     // matchConstruction: finals in order, then drop them from the queue
     uint32_t w = 0;
     for (uint32_t i = 0; i < count; i++) {
@@ -840,6 +878,8 @@ struct Lane {
       }
     }
     count = w;
+    CEP_PT(te4);
+    CEP_PACC(4, te4 - te2);
   }
 
   // ---------------------------------------------------------------- the key's stream
@@ -864,6 +904,7 @@ struct Lane {
   uint32_t pa_seq = 0;
 
   __device__ __forceinline__ bool tick() {
+    CEP_PT(tq0);
     bool known = false;
     if (q.quiet && A.bhits && only_begin()) {
       // the next event whose begin predicate holds or throws, 64 positions per word;
@@ -900,6 +941,8 @@ struct Lane {
       jj = h;
       known = true;  // the scan already found the begin predicate true
     }
+    CEP_PT(tq1);
+    CEP_PACC(1, tq1 - tq0);
     j = jj;
     if (ev_pos != jj) {
       q.load_ev(ev, base + jj);
@@ -925,22 +968,35 @@ struct Lane {
 
   // the whole key in one go (streaming sessions: one key per lane and launch)
   __device__ __forceinline__ void run() {
+    CEP_PT(tr0);
     jj = j0;
     jn = j0 + n_ev;
     pa_err = KE_OK;
     bool more = jj < jn;
     while (more) {
+      CEP_PACC(8, 1);
+      CEP_PT(tf0);
       if (A.defer && __any(wq_n >= kWalkFlush)) {
         flush();
         if (err) break;
       }
+      CEP_PT(tf1);
+      CEP_PACC(0, tf1 - tf0);
       more = tick();
     }
+    CEP_PT(tr1);
     if (pa_err != KE_OK || !err) {
       err = KE_OK;
       flush();  // every lane of the wave together
       finish_err();
     }
+#ifdef CEP_PROF
+    CEP_PT(tr2);
+    CEP_PACC(5, tr2 - tr1);
+    CEP_PACC(6, 1);
+    CEP_PACC(7, tr2 - tr0);
+    if (A.prof) prof_flush();
+#endif
   }
 
   // a fresh job: key `k`'s events of this batch from the NFA's initial state
@@ -1028,7 +1084,9 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   // at a time, so rounds mostly hand out a single job)
   constexpr uint32_t kClaim = 128;
   uint64_t wnext = 0, wend = 0;
+  CEP_PT(tr0);
   for (;;) {
+    CEP_LPACC(L, 8, 1);
     const uint64_t need = __ballot(!has && !drained);
     if (need) {
       if (wnext == wend) {
@@ -1059,6 +1117,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
     // drain when a queue is long, when kJobDrain lanes wait for their final drain, or when no
     // lane has events left to run (the finished lanes' drains batched into one flush)
     const uint64_t ending = __ballot(has && phase == 1);
+    CEP_PT(tf0);
     if (A.defer && (__any(has && L.wq_n >= kWalkFlush) ||
                     (ending && (__popcll(ending) >= kJobDrain || !__any(has && phase == 0))))) {
       L.flush();  // every lane of the wave together (lanes without a queue leave at once)
@@ -1068,6 +1127,8 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
         phase = 2;
       }
     }
+    CEP_PT(tf1);
+    CEP_LPACC(L, 0, tf1 - tf0);
     if (has && phase == 0 && !L.tick()) {
       // the events are over (or a step threw): the remaining walks drain at the next flush
       L.err = KE_OK;
@@ -1089,6 +1150,12 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
       has = false;
     }
   }
+#ifdef CEP_PROF
+  CEP_PT(tr1);
+  CEP_LPACC(L, 6, 1);
+  CEP_LPACC(L, 7, tr1 - tr0);
+  if (A.prof) L.prof_flush();
+#endif
 }
 
 // Driver shared by the AOT and JIT kernels: slot -> key, initial or carried state, the

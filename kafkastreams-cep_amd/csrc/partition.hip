@@ -12,7 +12,6 @@
 // workloads.generate interleaved round-robin, arrival order = (index within key, key).
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 
 #include "cep_internal.h"
 #include "kernel_args.h"
@@ -302,58 +301,6 @@ hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t
     tmp_bytes = need;
   }
   return lsd_sort(est, n, 32, true, 0, est_sorted, order, tmp, tmp_bytes, nullptr, st);
-}
-
-// ---- synthetic arrival order: CSR position p of key k, index j -> sort key j * n_keys + k
-__global__ void __launch_bounds__(256) arrival_keys(const uint64_t* __restrict__ key_off, uint64_t n_keys,
-                                                    uint64_t* skey, uint32_t* kid) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n_keys) return;
-  for (uint64_t p = key_off[k]; p < key_off[k + 1]; p++) {
-    skey[p] = (p - key_off[k]) * n_keys + k;
-    kid[p] = (uint32_t)k;
-  }
-}
-
-__global__ void __launch_bounds__(256) arrival_gather(const uint32_t* __restrict__ order, uint64_t n, const uint32_t* kid,
-                                                      const int32_t* c0, const int32_t* c1, uint32_t* key_out,
-                                                      int32_t* o0, int32_t* o1) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t p = order[i];
-  key_out[i] = kid[p];
-  o0[i] = c0[p];
-  if (c1) o1[i] = c1[p];
-}
-
-// CSR stream (key_off, c0, c1) -> arrival order (key_out, o0, o1), on the device
-hipError_t csr_to_arrival(const uint64_t* key_off, uint64_t n_keys, uint64_t n, uint64_t max_nk, const int32_t* c0,
-                          const int32_t* c1, uint32_t* key_out, int32_t* o0, int32_t* o1, hipStream_t st) {
-  if (n == 0 || n_keys == 0) return hipSuccess;
-  uint64_t *skey = nullptr, *skey2 = nullptr;
-  uint32_t *kid = nullptr, *idx = nullptr, *order = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  hipError_t e = hipSuccess;
-  auto ok = [&](hipError_t x) { if (e == hipSuccess) e = x; return e == hipSuccess; };
-  int bits = 1;  // sort keys < max_nk * n_keys
-  while (bits < 64 && (max_nk * n_keys) >> bits) bits++;
-  if (ok(hipMalloc(&skey, 8 * n)) && ok(hipMalloc(&skey2, 8 * n)) && ok(hipMalloc(&kid, 4 * n)) &&
-      ok(hipMalloc(&idx, 4 * n)) && ok(hipMalloc(&order, 4 * n))) {
-    hipLaunchKernelGGL(arrival_keys, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, key_off, n_keys, skey, kid);
-    hipLaunchKernelGGL(iota_u32, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, idx, n);
-    ok(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, skey, skey2, idx, order, (int)n, 0, bits, st));
-    if (ok(hipMalloc(&tmp, tmp_bytes + 256)) &&
-        ok(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, skey, skey2, idx, order, (int)n, 0, bits, st))) {
-      hipLaunchKernelGGL(arrival_gather, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, order, n, kid, c0, c1,
-                         key_out, o0, o1);
-      ok(hipGetLastError());
-      ok(hipStreamSynchronize(st));
-    }
-  }
-  for (void* p : {(void*)skey, (void*)skey2, (void*)kid, (void*)idx, (void*)order, tmp})
-    if (p) (void)hipFree(p);
-  return e;
 }
 
 }  // namespace cep

@@ -1,5 +1,7 @@
 // session.cpp — the C ABI (include/cep.h): query compile, sessions on one GPU, batch
-// matching, result retrieval.  Host code; kernels live in nfa.hip / stencil.hip / synth.hip.
+// matching, result retrieval.  Host code; kernels live in nfa.hip / stencil.hip / partition.hip /
+// ingest.hip / symbol.hip / shard.hip / watermark.hip (the synthetic generators of the bench
+// and the tests are a separate library, synth_gen.hip -> libcep_synth.so).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -200,6 +202,7 @@ struct cep_session {
   // scratch
   DBuf heavy;  // heavy-key list of the output scatter
   DBuf rings, walks, nodes, preds, preds0, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
+  DBuf prof;  // measurement runs ($CEP_PROF): the main launch's time split (nfa_lane.h)
 };
 
 namespace {
@@ -266,9 +269,15 @@ void run_stencil(cep_session* s, QueryRt& r) {
   s->bnd.ensure(sizeof(uint32_t) * (s->n_events / 64 + 2));                       // word -> key
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
+  if (!r.h_sc) HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocMapped));
+  if (s->n_events == 0) {
+    // launch_stencil launches nothing, so nothing writes this batch's count into the pinned
+    // copy: zero it here, once an earlier batch's stencil_emit can no longer overwrite it
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    r.h_sc->total = 0;
+  }
   r.m_key.ensure(sizeof(uint32_t) * cap);
   r.p_seq.ensure(sizeof(uint32_t) * cap * m);
-  if (!r.h_sc) HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocMapped));
   if (!r.tev[0][0])
     for (auto& t : r.tev)
       for (auto& e : t) HIPCHECK(hipEventCreate(&e));
@@ -505,6 +514,12 @@ void run_nfa(cep_session* s, GroupRt& g) {
   } else {
     g.est_valid = false;
   }
+  const bool prof = std::getenv("CEP_PROF") != nullptr;  // (the query must be compiled with it too)
+  if (prof) {
+    s->prof.ensure(16 * sizeof(unsigned long long));
+    HIPCHECK(hipMemsetAsync(s->prof.p, 0, 16 * sizeof(unsigned long long), s->stream));
+    a.prof = s->prof.as<unsigned long long>();
+  }
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
   HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
@@ -512,6 +527,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
   Scratch h{};
   HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
+  if (prof) {  // one line per launch on stderr: the counters of nfa_lane.h's CEP_PROF list
+    unsigned long long pc[16];
+    HIPCHECK(hipMemcpy(pc, s->prof.p, sizeof pc, hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "cep_prof {\"jobs\": %llu, \"c\": [", (unsigned long long)jobs);
+    for (int i = 0; i < 12; i++) std::fprintf(stderr, "%s%llu", i ? ", " : "", pc[i]);
+    std::fprintf(stderr, "]}\n");
+    a.prof = nullptr;
+  }
   float ms = 0;
   HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   total_ms += ms;
@@ -838,6 +861,25 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
   return CEP_OK;
 }
 
+int cep_session_reset(cep_session* s) {
+  if (!s) return fail(CEP_E_INVALID, "null session");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    for (auto& r : s->qs) {
+      StreamState& S = r->st;
+      if (!S.init) continue;
+      // KeyCarry.live = 0: each key restarts from the initial state at its next batch (its ring
+      // slots are rewritten from scratch); empty pools
+      HIPCHECK(hipMemsetAsync(S.carry.p, 0, sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1), s->stream));
+      HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
+      S.node_used = S.pred_used = 0;
+    }
+    s->watermark = INT64_MIN;
+    HIPCHECK(hipStreamSynchronize(s->stream));
+  });
+}
+
 void cep_session_destroy(cep_session* s) {
   if (!s) return;
   {
@@ -959,6 +1001,9 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       } else {
         s->ts = nullptr;
       }
+      // host buffers are borrowed for the call only: the copies (truly asynchronous from pinned
+      // memory) must be done before returning, even when only stencil work follows
+      HIPCHECK(hipStreamSynchronize(s->stream));
     }
     // watermark
     s->watermark = INT64_MIN;
@@ -972,7 +1017,10 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       HIPCHECK(hipMemcpyAsync(s->h_wm, &sc->wmax, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
       s->wm_pending = true;
     }
-    if (s->groups.size() && (uint64_t)s->qs.size() * s->n_keys >= 0xFFFFFFFFull)
+    // persistent lanes claim job indices 128 at a time from a u32 counter (nfa_lane.h
+    // run_jobs): every resident wave (at most 64 per CU) may claim up to 128 past the last job
+    const uint64_t claim_slack = (uint64_t)s->cus * 64 * 128;
+    if (s->groups.size() && (uint64_t)s->qs.size() * s->n_keys + claim_slack >= 0xFFFFFFFFull)
       throw std::invalid_argument("queries x keys of a batch must stay below 2^32 (job ids are u32)");
     for (auto& r : s->qs)  // a stream carries NFA state between batches: stencil queries run on the NFA there
       if (r->group < 0) run_stencil(s, *r);
@@ -1396,77 +1444,6 @@ int cep_memcpy(void* dst, const void* src, size_t bytes, int dst_memory, int src
   return guarded([&] { HIPCHECK(hipMemcpy(dst, src, bytes, k)); });
 }
 
-// ---- synthetic workloads ----
-static std::vector<uint64_t> synth_offsets(int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
-                                           uint32_t mean) {
-  (void)kind;
-  std::vector<uint64_t> off(n_keys + 1, 0);
-  const uint64_t sp = (uint64_t)std::floor(std::sqrt((double)mean));
-  for (uint64_t k = 0; k < n_keys; k++) {
-    const uint64_t h = cep::synth_hash_host(seed, k + key_base, 0xFFFFFFFFull);
-    off[k + 1] = off[k] + (mean - sp + h % (2 * sp + 1));
-  }
-  return off;
-}
-
-int cep_synth_count(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, uint32_t mean_events,
-                    uint64_t* n_events) {
-  (void)device;
-  if (!n_events || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
-  *n_events = synth_offsets(kind, seed, n_keys, key_base, mean_events)[n_keys];
-  return CEP_OK;
-}
-
-int cep_synth_generate(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base, uint32_t mean_events,
-                       uint64_t* key_off_dev, int32_t* const* cols_dev) {
-  if (!key_off_dev || !cols_dev || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
-  if (kind != 0 && kind != 1) return fail(CEP_E_INVALID, "kind must be 0 (abc) or 1 (stock)");
-  return guarded([&] {
-    DeviceGuard g(device);
-    HIPCHECK(hipSetDevice(device));
-    auto off = synth_offsets(kind, seed, n_keys, key_base, mean_events);
-    HIPCHECK(hipMemcpy(key_off_dev, off.data(), sizeof(uint64_t) * (n_keys + 1), hipMemcpyHostToDevice));
-    HIPCHECK(launch_synth(kind, seed, n_keys, key_base, key_off_dev, cols_dev[0], kind == 1 ? cols_dev[1] : nullptr,
-                          nullptr));
-    HIPCHECK(hipDeviceSynchronize());
-  });
-}
-
-int cep_synth_ts(int device, uint64_t n_events, int64_t base, int64_t* ts_dev) {
-  if (!ts_dev && n_events) return fail(CEP_E_INVALID, "null argument");
-  return guarded([&] {
-    DeviceGuard g(device);
-    HIPCHECK(hipSetDevice(device));
-    HIPCHECK(launch_synth_ts(ts_dev, n_events, base, nullptr));
-    HIPCHECK(hipDeviceSynchronize());
-  });
-}
-
-int cep_synth_generate_arrival(int device, int kind, uint64_t seed, uint64_t n_keys, uint64_t key_base,
-                               uint32_t mean_events, uint32_t* keys_dev, int32_t* const* cols_dev) {
-  if (!keys_dev || !cols_dev || mean_events == 0) return fail(CEP_E_INVALID, "bad argument");
-  if (kind != 0 && kind != 1) return fail(CEP_E_INVALID, "kind must be 0 (abc) or 1 (stock)");
-  return guarded([&] {
-    DeviceGuard g(device);
-    HIPCHECK(hipSetDevice(device));
-    auto off = synth_offsets(kind, seed, n_keys, key_base, mean_events);
-    const uint64_t n = off[n_keys];
-    uint64_t max_nk = 1;
-    for (uint64_t k = 0; k < n_keys; k++) max_nk = std::max<uint64_t>(max_nk, off[k + 1] - off[k]);
-    DBuf d_off, c0, c1;
-    d_off.ensure(8 * (n_keys + 1));
-    c0.ensure(4 * std::max<uint64_t>(n, 1));
-    if (kind == 1) c1.ensure(4 * std::max<uint64_t>(n, 1));
-    HIPCHECK(hipMemcpy(d_off.p, off.data(), 8 * (n_keys + 1), hipMemcpyHostToDevice));
-    HIPCHECK(launch_synth(kind, seed, n_keys, key_base, d_off.as<uint64_t>(), c0.as<int32_t>(),
-                          kind == 1 ? c1.as<int32_t>() : nullptr, nullptr));
-    HIPCHECK(csr_to_arrival(d_off.as<uint64_t>(), n_keys, n, max_nk, c0.as<int32_t>(),
-                            kind == 1 ? c1.as<int32_t>() : nullptr, keys_dev, cols_dev[0],
-                            kind == 1 ? cols_dev[1] : nullptr, nullptr));
-    HIPCHECK(hipDeviceSynchronize());
-  });
-}
-
 int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_off, uint64_t n_records,
                           int col_width, void* price, void* volume, int32_t* status, uint32_t* name_span,
                           void* stream) {
@@ -1497,20 +1474,11 @@ int cep_symbol_keys(int device, const uint8_t* bytes, const uint64_t* rec_off, c
   });
   if (rc) return rc;
   if (err & 1u) return fail(CEP_E_INVALID, "a record's name holds malformed UTF-8");
-  if (err & 2u) return fail(CEP_E_INVALID, "more distinct names than max_symbols");
+  // (the hash table holds at least 2 x max_symbols slots: err bit 2 only fires when it is
+  // full, so the limit itself is checked on the count)
+  if ((err & 2u) || *n_symbols > max_symbols) return fail(CEP_E_INVALID, "more distinct names than max_symbols");
   if (err & 4u) return fail(CEP_E_INVALID, "64-bit hash collision between two different names");
   return CEP_OK;
-}
-
-int cep_synth_stock_json(int device, const int32_t* price_dev, const int32_t* volume_dev, uint64_t n,
-                         uint8_t* out_dev, uint64_t cap, uint64_t* rec_off_dev, uint64_t* total) {
-  if (!rec_off_dev || !total || (n && (!price_dev || !volume_dev))) return fail(CEP_E_INVALID, "null argument");
-  if (n >= (1ull << 31)) return fail(CEP_E_INVALID, "at most 2^31 - 1 records");
-  return guarded([&] {
-    DeviceGuard g(device);
-    HIPCHECK(hipSetDevice(device));
-    HIPCHECK(synth_stock_json(price_dev, volume_dev, n, out_dev, out_dev ? cap : 0, rec_off_dev, total));
-  });
 }
 
 }  // extern "C"

@@ -11,6 +11,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcep.so")
+SYNTH_LIB_PATH = os.path.join(_HERE, "libcep_synth.so")  # bench/test generators (include/cep_synth.h)
 
 CEP_MEM_HOST, CEP_MEM_DEVICE = 0, 1
 CEP_KIND_NFA, CEP_KIND_STENCIL = 0, 1
@@ -24,11 +25,14 @@ EXPORTS = [
     "cep_session_create", "cep_session_destroy", "cep_push_batch", "cep_sync", "cep_poll_matches",
     "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
-    "cep_synth_count", "cep_synth_generate", "cep_query_jit_source", "cep_jit_precompile",
-    "cep_batch_layout", "cep_synth_generate_arrival", "cep_session_snapshot", "cep_session_restore",
-    "cep_decode_stock_json", "cep_synth_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
-    "cep_last_stats", "cep_gather_keys", "cep_synth_ts", "cep_timing_totals", "cep_symbol_keys", "cep_lane_balance",
+    "cep_query_jit_source", "cep_jit_precompile", "cep_session_reset",
+    "cep_batch_layout", "cep_session_snapshot", "cep_session_restore",
+    "cep_decode_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
+    "cep_last_stats", "cep_gather_keys", "cep_timing_totals", "cep_symbol_keys", "cep_lane_balance",
 ]
+# every symbol include/cep_synth.h declares (the generator library of the bench and tests)
+SYNTH_EXPORTS = ["cep_synth_last_error", "cep_synth_count", "cep_synth_generate", "cep_synth_generate_arrival",
+                 "cep_synth_ts", "cep_synth_stock_json"]
 
 
 class QueryInfo(C.Structure):
@@ -98,20 +102,16 @@ def lib():
                                   C.c_int),
             "cep_last_error": ([], C.c_char_p),
             "cep_last_stats": ([vp, C.c_int, C.POINTER(BatchStats)], C.c_int),
-            "cep_synth_ts": ([C.c_int, u64, C.c_int64, vp], C.c_int),
             "cep_gather_keys": ([C.c_int, u64, vp, vp, vp, C.c_int, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp),
                                  vp, vp], C.c_int),
             "cep_device_alloc": ([C.c_int, C.c_size_t, C.POINTER(vp)], C.c_int),
             "cep_device_free": ([vp], C.c_int),
             "cep_memcpy": ([vp, vp, C.c_size_t, C.c_int, C.c_int], C.c_int),
-            "cep_synth_count": ([C.c_int, C.c_int, u64, u64, u64, u32, C.POINTER(u64)], C.c_int),
-            "cep_synth_generate": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
-            "cep_synth_generate_arrival": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
             "cep_batch_layout": ([vp, C.c_int, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_double)], C.c_int),
             "cep_session_snapshot": ([vp, vp, C.c_size_t, C.POINTER(C.c_size_t)], C.c_int),
             "cep_session_restore": ([vp, vp, C.c_size_t], C.c_int),
+            "cep_session_reset": ([vp], C.c_int),
             "cep_decode_stock_json": ([C.c_int, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
-            "cep_synth_stock_json": ([C.c_int, vp, vp, u64, vp, u64, vp, C.POINTER(u64)], C.c_int),
             "cep_symbol_keys": ([C.c_int, vp, vp, vp, vp, u64, u64, vp, C.POINTER(u64), vp], C.c_int),
             "cep_lane_balance": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
         }
@@ -120,6 +120,38 @@ def lib():
             f.argtypes, f.restype = args, res
         _lib = L
     return _lib
+
+
+_synth = None
+
+
+def synth_lib():
+    """libcep_synth.so: the synthetic generators (bench and tests only; the matcher never
+    loads it)."""
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_LIB_PATH):
+            raise RuntimeError(f"{SYNTH_LIB_PATH} is missing: run __graft_entry__.build()")
+        L = C.CDLL(SYNTH_LIB_PATH)
+        vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
+        sig = {
+            "cep_synth_last_error": ([], C.c_char_p),
+            "cep_synth_ts": ([C.c_int, u64, C.c_int64, vp], C.c_int),
+            "cep_synth_count": ([C.c_int, C.c_int, u64, u64, u64, u32, C.POINTER(u64)], C.c_int),
+            "cep_synth_generate": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
+            "cep_synth_generate_arrival": ([C.c_int, C.c_int, u64, u64, u64, u32, vp, C.POINTER(vp)], C.c_int),
+            "cep_synth_stock_json": ([C.c_int, vp, vp, u64, vp, u64, vp, C.POINTER(u64)], C.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes, f.restype = args, res
+        _synth = L
+    return _synth
+
+
+def _check_synth(rc):
+    if rc != 0:
+        raise CepError(f"libcep_synth error {rc}: {synth_lib().cep_synth_last_error().decode(errors='replace')}")
 
 
 class CepError(RuntimeError):
@@ -246,22 +278,22 @@ class DeviceStream:
 
 def synth_stream(kind: str, seed: int, n_keys: int, mean_events: int, key_base: int = 0,
                  device: int = 0) -> DeviceStream:
-    """Generate workloads.SynthConfig data directly in HBM (csrc/synth.hip)."""
+    """Generate workloads.SynthConfig data directly in HBM (csrc/synth_gen.hip, libcep_synth.so)."""
     k = {"abc": 0, "stock": 1}[kind]
     n = C.c_uint64()
-    _check(lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
+    _check_synth(synth_lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
     off = DeviceBuffer(8 * (n_keys + 1), device)
     ncols = 1 if k == 0 else 2
     cols = [DeviceBuffer(4 * max(1, n.value), device) for _ in range(ncols)]
     ptrs = (C.c_void_p * ncols)(*[c.ptr for c in cols])
-    _check(lib().cep_synth_generate(device, k, seed, n_keys, key_base, mean_events, off.ptr, ptrs))
+    _check_synth(synth_lib().cep_synth_generate(device, k, seed, n_keys, key_base, mean_events, off.ptr, ptrs))
     return DeviceStream(n_keys, n.value, off, cols, device)
 
 
 def synth_ts(n_events: int, base: int = 1_600_000_000_000, device: int = 0) -> "DeviceBuffer":
     """Device timestamps base + CSR position for a synthetic stream (cep_synth_ts)."""
     b = DeviceBuffer(8 * max(1, n_events), device)
-    _check(lib().cep_synth_ts(device, n_events, base, b.ptr))
+    _check_synth(synth_lib().cep_synth_ts(device, n_events, base, b.ptr))
     return b
 
 
@@ -288,6 +320,37 @@ def shard_stream(stream: "DeviceStream", keys: np.ndarray, local_off: np.ndarray
     return DeviceStream(len(keys), n, off, cols, stream.device), dts
 
 
+def gather_ranges(stream: "DeviceStream", starts: np.ndarray, ends: np.ndarray) -> "DeviceStream":
+    """A new CSR stream whose key k holds positions [starts[k], ends[k]) of `stream` (device
+    gather, cep_gather_keys with a source-offset table of (start, end) pairs: key k reads
+    src_off[2k] .. src_off[2k + 1]).  Used to cut a stream into consecutive per-key slices,
+    the batches of a streaming session."""
+    starts = np.ascontiguousarray(starts, np.uint64)
+    ends = np.ascontiguousarray(ends, np.uint64)
+    nk = len(starts)
+    pairs = np.empty(2 * nk, np.uint64)
+    pairs[0::2] = starts
+    pairs[1::2] = ends
+    local = np.zeros(nk + 1, np.uint64)
+    np.cumsum(ends - starts, out=local[1:])
+    n = int(local[-1])
+    sel = DeviceBuffer(max(4, 4 * nk), stream.device)
+    if nk:
+        sel.upload((2 * np.arange(nk, dtype=np.uint64)).astype(np.uint32))
+    src = DeviceBuffer(max(8, pairs.nbytes), stream.device)
+    if nk:
+        src.upload(pairs)
+    off = DeviceBuffer(local.nbytes, stream.device)
+    off.upload(local)
+    cols = [DeviceBuffer(4 * max(1, n), stream.device) for _ in stream.cols]
+    nc = len(cols)
+    widths = (C.c_uint32 * nc)(*([4] * nc))
+    sp = (C.c_void_p * nc)(*[c.ptr for c in stream.cols])
+    dp = (C.c_void_p * nc)(*[c.ptr for c in cols])
+    _check(lib().cep_gather_keys(stream.device, nk, sel.ptr, src.ptr, off.ptr, nc, widths, sp, dp, None, None))
+    return DeviceStream(nk, n, off, cols, stream.device)
+
+
 class ArrivalStream:
     """A device-resident arrival-order batch: the key of every event + int32 columns."""
 
@@ -304,11 +367,11 @@ def synth_arrival_stream(kind: str, seed: int, n_keys: int, mean_events: int, ke
     """workloads.generate_arrival's stream, generated in HBM (csrc/partition.hip)."""
     k = {"abc": 0, "stock": 1}[kind]
     n = C.c_uint64()
-    _check(lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
+    _check_synth(synth_lib().cep_synth_count(device, k, seed, n_keys, key_base, mean_events, C.byref(n)))
     keys = DeviceBuffer(4 * max(1, n.value), device)
     cols = [DeviceBuffer(4 * max(1, n.value), device) for _ in range(1 if k == 0 else 2)]
     ptrs = (C.c_void_p * len(cols))(*[c.ptr for c in cols])
-    _check(lib().cep_synth_generate_arrival(device, k, seed, n_keys, key_base, mean_events, keys.ptr, ptrs))
+    _check_synth(synth_lib().cep_synth_generate_arrival(device, k, seed, n_keys, key_base, mean_events, keys.ptr, ptrs))
     return ArrivalStream(n_keys, n.value, keys, cols, device)
 
 
@@ -337,9 +400,9 @@ class StockJsonBatch:
         """json-simple's serialization of n StockEvents e1..en (csrc/ingest.hip), made in HBM."""
         o = DeviceBuffer(8 * (n + 1), device)
         tot = C.c_uint64()
-        _check(lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, None, 0, o.ptr, C.byref(tot)))
+        _check_synth(synth_lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, None, 0, o.ptr, C.byref(tot)))
         d = DeviceBuffer(max(1, tot.value), device)
-        _check(lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, d.ptr, tot.value, o.ptr, C.byref(tot)))
+        _check_synth(synth_lib().cep_synth_stock_json(device, price.ptr, volume.ptr, n, d.ptr, tot.value, o.ptr, C.byref(tot)))
         return cls(n, tot.value, d, o, device)
 
     def download(self):
@@ -537,6 +600,11 @@ class Session:
         st = BatchStats()
         _check(lib().cep_last_stats(self.h, query, C.byref(st)))
         return {k: getattr(st, k) for k, _ in BatchStats._fields_}
+
+    def reset(self) -> None:
+        """cep_session_reset: every key of a streaming session back to the NFA's initial
+        state (allocations kept)."""
+        _check(lib().cep_session_reset(self.h))
 
     def snapshot(self) -> bytes:
         """The streaming session's complete per-key NFA state as a versioned blob

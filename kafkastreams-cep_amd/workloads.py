@@ -8,7 +8,7 @@ Synthetic streams are generated directly in key-partitioned (CSR) form: key k ho
 events (mean M, spread ±⌊√M⌋, like a uniform key hash would give), and every event value
 is a counter-based SplitMix64 hash of (seed, key, index-in-key), so any subset of keys can
 be regenerated independently (the CPU-baseline sample) and the GPU generator
-(csrc/synth.hip) reproduces this module bit for bit.  Event id = CSR position.
+(csrc/synth_gen.hip) reproduces this module bit for bit.  Event id = CSR position.
 """
 from __future__ import annotations
 
@@ -61,18 +61,34 @@ def strict_abc_query(schema: EventSchema | None = None):
             .select("C").where(lambda k, v, ts, s: v.v >= 8).build())
 
 
-def any_kleene_query(schema: EventSchema | None = None):
-    """Config 4: skip_till_any Kleene+ with folds and a tight WITHIN (run-explosion stress)."""
+def any_kleene_query(schema: EventSchema | None = None, carry_volume: bool = False):
+    """Config 4: skip_till_any Kleene+ with folds and a tight WITHIN (run-explosion stress).
+
+    As written the query throws NullPointerException in the reference on
+    about half of the keys: a branched run copies only the current stage's aggregates
+    (NFA.java:243, ValueStore.java:92-97), so S2's `state.get("volume")` reads null on every
+    run branched at S1.  `carry_volume=True` is the stress workload SURVEY §8d intends ("no
+    Appendix-C exception path fires"): S1 also folds `volume` (keeping its value), so a
+    branch at S1 copies it, and S2 reads it with `getOrElse("volume", 0)` (a run branched at
+    S2, which has no aggregates, carries no folds at all).  No key throws; runs accumulate at
+    S1/S2 and orphan buffer nodes grow.  Oracle, keys 0, 500, ...: 0 of 2000 keys
+    throw, up to 23 live runs and 1003 buffer nodes per key, 1566 matches.  The literal query
+    stays the parity case."""
     schema = schema or EventSchema({"price": "int", "volume": "int"})
-    return (QueryBuilder(schema)
-            .select("S0").where(lambda k, v, ts, s: v.volume > 1000)
-            .fold("avg", lambda k, v, c: v.price).fold("volume", lambda k, v, c: v.volume).then()
-            .select("S1").oneOrMore().skipTillAnyMatch()
-            .where(lambda k, v, ts, s: v.price > s.get("avg"))
-            .fold("avg", lambda k, v, c: (c + v.price) / 2).fold("sum", lambda k, v, c: v.price, type="int").then()
-            .select("S2").skipTillAnyMatch()
-            .where(lambda k, v, ts, s: v.volume * 5 < 4 * s.get("volume"))
-            .within(10, TimeUnit.MILLISECONDS).build())
+    s1 = (QueryBuilder(schema)
+          .select("S0").where(lambda k, v, ts, s: v.volume > 1000)
+          .fold("avg", lambda k, v, c: v.price).fold("volume", lambda k, v, c: v.volume).then()
+          .select("S1").oneOrMore().skipTillAnyMatch()
+          .where(lambda k, v, ts, s: v.price > s.get("avg"))
+          .fold("avg", lambda k, v, c: (c + v.price) / 2).fold("sum", lambda k, v, c: v.price, type="int"))
+    if carry_volume:
+        s1 = s1.fold("volume", lambda k, v, c: c)
+    s2 = s1.then().select("S2").skipTillAnyMatch()
+    if carry_volume:
+        s2 = s2.where(lambda k, v, ts, s: v.volume * 5 < 4 * s.getOrElse("volume", 0))
+    else:
+        s2 = s2.where(lambda k, v, ts, s: v.volume * 5 < 4 * s.get("volume"))
+    return s2.within(10, TimeUnit.MILLISECONDS).build()
 
 
 def multi_queries(n: int = 64):

@@ -15,7 +15,7 @@ def _irs(bench_only):
     from kafkastreams_cep_amd import workloads as W
 
     irs = [W.stock_query(v).to_ir() for v in ("readme", "test", "demo")]
-    irs += [W.strict_abc_query().to_ir(), W.any_kleene_query().to_ir()]
+    irs += [W.strict_abc_query().to_ir(), W.any_kleene_query().to_ir(), W.any_kleene_query(carry_volume=True).to_ir()]
     irs += [p.to_ir() for p in W.multi_queries(64)]  # bench.py other_configs (cfg 5); tests use the first 8
     # semantic WITHIN (tests/test_semantic_within.py, bench.py semantic figure)
     irs += [q.to_ir(semantic_within=True) for q in (W.stock_query("readme"), W.stock_query("test"),

@@ -14,20 +14,31 @@ from kafkastreams_cep_amd import workloads as W
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "cep.h")).read()
+def header_functions(header="cep.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(cep_[a-z_]+)\s*\(", src)))
 
 
 def test_header_exports_match_binding():
     assert header_functions() == sorted(N.EXPORTS)
+    assert header_functions("cep_synth.h") == sorted(N.SYNTH_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol():
     L = N.lib()
     for name in header_functions():
         assert hasattr(L, name), name
+    G = N.synth_lib()
+    for name in header_functions("cep_synth.h"):
+        assert hasattr(G, name), name
+
+
+def test_matcher_library_carries_no_generators():
+    """the synthetic generators (and their hipCUB sorts/scans) live in libcep_synth.so only"""
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "-C", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "cep_synth" not in syms and "hipcub" not in syms.lower() and "rocprim" not in syms.lower()
 
 
 def test_compile_kinds():
