@@ -247,6 +247,13 @@ int cep_watermark(cep_session* s, int64_t* out);
  * next cep_push_batch continues every key's stream where the snapshot left it.  Blobs from
  * other queries, options or versions are rejected with CEP_E_INVALID before any change. */
 int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size);
+
+/* Streaming sessions: floor[k] = the smallest sequence number of key k's events that a live
+ * node of the query's shared buffer still holds (0xFFFFFFFF: none) - the only events a later
+ * match of the key can contain (KVSharedVersionedBuffer.java:143-171 deletes a node when its
+ * last reference is walked).  A host that keeps records to build Sequences may drop the older
+ * ones.  floor is host memory [n_keys]; n_keys <= the session's key space. */
+int cep_live_floor(cep_session* s, int query, uint32_t* floor, uint64_t n_keys);
 int cep_session_restore(cep_session* s, const void* buf, size_t size);
 
 int cep_last_timing(cep_session* s, int query, double* kernel_ms, double* aux_ms, uint32_t* launches);

@@ -83,7 +83,12 @@ hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_of
                                     void* price, void* volume, int32_t* status, uint32_t* name_span,
                                     hipStream_t st);
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
+struct Node;
+hipError_t launch_live_floor(const Node* nodes, uint64_t n_nodes, uint64_t n_keys, uint32_t* floor, hipStream_t st);
 std::vector<char> jit_code_object(const std::string& src, double* compile_s);
+// the wide build of a generated kernel (6 Dewey pairs; the source as generated is the narrow
+// build): capacity re-runs and streaming sessions run it
+inline std::string jit_wide_source(const std::string& src) { return "#define CEP_DEWEY_PAIRS 6\n" + src; }
 struct Cols;
 size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,

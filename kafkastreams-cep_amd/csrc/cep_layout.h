@@ -20,7 +20,12 @@ constexpr int kMaxFields = 16;
 constexpr int kMaxStates = 8;      // fold state names per query (MAXF)
 constexpr int kMaxAggs = 8;        // folds per pattern
 constexpr int kMaxStack = 16;      // interpreter stack depth
-constexpr int kDeweyPairs = 6;     // RLE pairs per Dewey version (overflow -> CEP_KEY_CAPACITY)
+// RLE pairs per Dewey version (overflow -> CEP_KEY_CAPACITY).  A generated kernel may be
+// compiled with fewer ($CEP_DEWEY_PAIRS, measurement runs); host-side sizes always use 6.
+#ifndef CEP_DEWEY_PAIRS
+#define CEP_DEWEY_PAIRS 6
+#endif
+constexpr int kDeweyPairs = CEP_DEWEY_PAIRS;
 constexpr int kMaxStencil = 8;     // stages of a CEP_KIND_STENCIL query (stencil.hip instantiations)
 
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
@@ -83,13 +88,14 @@ struct Rec {
   uint32_t stage;
   uint32_t event;     // sequence number of the run's last event within the key, CEP_NONE = null
   uint32_t ev_first;  // head of the node chain of `event` (CEP_NONE: none / pending)
+  uint32_t node;      // the node (source stage key, event) when known and valid (nfa_lane.h), else CEP_NONE
   uint32_t nullmask;  // bit s: fold state s is null
   Dewey ver;
   int64_t fold[F];
 };
 
 // ---- buffer node (TimedKeyValue + its StackEventKey, nfa/buffer/impl/TimedKeyValue.java)
-// Two 16-B quads, read and written as vectors: {event, refs, head, tail}, {same_next, meta, lk, -}
+// Two 16-B quads, read and written as vectors: {event, refs, head, tail}, {same_next, meta, lk, key}
 struct alignas(16) Node {
   uint32_t event;      // sequence number within key
   int32_t refs;        // TimedKeyValue.refs
@@ -97,7 +103,7 @@ struct alignas(16) Node {
   uint32_t same_next;  // next node created at the same event (lookup chain)
   uint32_t meta;       // [7:0] stage key, bit8 live, [31:16] live predecessor count
   uint32_t lk;         // walks queued when put() last found this node live (deferred walks)
-  uint32_t pad;
+  uint32_t key;        // the key (job key) whose NFA made the node (cep_live_floor)
 };
 
 // pointer ids: kPred0 | node = the node's first-pointer slot (preds0[node]), else the pool

@@ -532,11 +532,19 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     for (auto& a : *sa.second) uses(a.second.get(), fields, ts);
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
-  o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
-  // tuning knobs of nfa_lane.h, for measurement runs only ($CEP_WALK_FLUSH, $CEP_QUIET_CHUNK)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF"})
+  // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
+  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
+  // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:
+  // every run of the bench configs fits, SURVEY §8d sample); a job whose version would need
+  // more reports KE_RETRY and is re-run by the wide build of the same source (6 pairs:
+  // jit_wide_source), which also runs streaming sessions.  ($CEP_DEWEY_PAIRS: measurement runs)
+  int narrow = 3;
+  if (const char* v = std::getenv("CEP_DEWEY_PAIRS"))
+    if (std::atoi(v) > 0) narrow = std::atoi(v);
+  o += "#ifndef CEP_DEWEY_PAIRS\n#define CEP_DEWEY_PAIRS " + std::to_string(narrow) + "\n#endif\n";
+  o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
   if (lits.param) o += "#define CEP_WALK_COMPAT2 1  // kernel group: the wider straight-line walk step\n";
   o += "#include \"dewey.h\"\n#include \"java.h\"\n#include \"nfa_lane.h\"\n\nnamespace cep {\nnamespace {\n\n";
   o += "constexpr int F = " + std::to_string(F) + ";\n";
@@ -545,7 +553,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     if (fields[f]) o += "  " + std::string(ctype(d.field_type[f])) + " f" + std::to_string(f) + ";\n";
   o += "  int64_t ts;\n};\n";
   o += "struct Fo {\n  int64_t v[F];\n  uint32_t nm;\n};\n";
-  o += "struct Top {\n  uint32_t stage, event, ev_first;\n};\n";
+  o += "struct Top {\n  uint32_t stage, event, ev_first, node, hsk;  // node hint of (hsk, event)\n};\n";
   o += "struct Out {\n  int produced;\n  int same;  // slot of the output record that keeps the run's sequence id\n};\n\n";
   // the begin predicate's own columns (the quiet scan loads only these)
   std::vector<bool> bfields(d.n_fields, false);
@@ -705,28 +713,31 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       const std::string m = "m" + std::to_string(e);
       if (E.op == OP_TAKE) {
         f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver);\n";
+        f += "        const uint32_t nd = L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n";
+        f += "        if (L.err) return;\n";
+        f += "        const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver, nd);\n";
         f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n";
-        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      } else {\n";
-        f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
-        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2);\n      }\n";
+        f += "      } else {\n";
+        f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = kDwFull; return; }\n";
+        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2, top.hsk, top.node);\n      }\n";
         f += "      if (L.err) return;\n      consumed = true;\n    }\n";
       } else if (E.op == OP_BEGIN) {
         const bool fin = d.st[E.target].type == ST_FINAL;
-        f += "    if (" + m + ") {\n      L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n";
+        f += "    if (" + m + ") {\n      const uint32_t nd = L.put_link(" + SK +
+             ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n      if (L.err) return;\n";
         f += "      const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
-             (fin ? " | kRecFinal" : "") + ", L.j, CEP_NONE, ver);\n";
+             (fin ? " | kRecFinal" : "") + ", L.j, CEP_NONE, ver, nd);\n";
         f += "      if (r < 0) return;\n      o.same = r;\n      o.produced++;\n      consumed = true;\n    }\n";
       } else if (E.op == OP_IGNORE) {
         f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        const int r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver);\n";
+        f += "        const int r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver, top.node);\n";
         f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n      }\n      ignored = true;\n    }\n";
       } else {  // PROCEED
         const DevStage& T = d.st[E.target];
         const std::string TI = std::to_string(E.target);
         f += "    if (" + m + ") {\n";
         if (T.sk != S.sk) {
-          f += "      if (!branching) {\n        Dewey v2 = ver;\n        if (!dw_add_stage(v2)) { L.err = KE_CAPACITY; return; }\n";
+          f += "      if (!branching) {\n        Dewey v2 = ver;\n        if (!dw_add_stage(v2)) { L.err = kDwFull; return; }\n";
           f += "        E" + TI + "(L, top, v2, false, " + SK + ", ev, w, o);\n      } else {\n";
           f += "        E" + TI + "(L, top, ver, true, " + SK + ", ev, w, o);\n      }\n";
         } else {
@@ -736,9 +747,9 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       }
     }
     f += "    if (br) {\n      if (prev_sk == kNoSk) { L.err = KE_NPE; return; }\n";
-    f += "      Dewey v2 = ver;\n      if (!dw_add_run(v2)) { L.err = KE_CAPACITY; return; }\n";
+    f += "      Dewey v2 = ver;\n      if (!dw_add_run(v2)) { L.err = kDwFull; return; }\n";
     f += "      const int r = L.push_rec(kRecEps | kRecBranch | (prev_sk << 8) | " + SI +
-         "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2);\n      if (r < 0) return;\n";
+         "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2, ignored && prev_sk == top.hsk ? top.node : CEP_NONE);\n      if (r < 0) return;\n";
     f += "      uint32_t nm = (1u << F) - 1;\n      int64_t fv[F];\n      for (int s = 0; s < F; s++) fv[s] = 0;\n";
     for (int a = 0; a < S.n_aggs; a++) {
       const std::string si = std::to_string(S.agg_state[a]);
@@ -770,14 +781,14 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "        if (win != -1 && ev.ts - start > win) return 0;\n      }\n";
     o += "      w.v[FS] = (int64_t)(uint32_t)(uint64_t)start;\n      w.v[FS + 1] = (int64_t)(uint32_t)((uint64_t)start >> 32);\n    }\n";
   }
-  o += "    const Top top{c.stage, c.event, c.ev_first};\n    Out o{0, -1};\n";
+  o += "    const Top top{c.stage, c.event, c.ev_first, c.node, (c.stage & kRecEps) ? ((c.stage >> 8) & 0xFFu) : kNoSk};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
   o += "    if (c.stage & kRecEps) {\n      const uint32_t esk = (c.stage >> 8) & 0xFF;\n      switch (c.stage & 0xFF) {\n";
   for (uint32_t s = 0; s < d.n_stages; s++) {
     if (d.st[s].type == ST_FINAL) continue;
     const std::string SI = std::to_string(s), SK = std::to_string(d.st[s].sk);
     o += "        case " + SI + ":\n          if (esk != " + SK + "u && !brf) {\n            Dewey v2 = c.ver;\n";
-    o += "            if (!dw_add_stage(v2)) { L.err = KE_CAPACITY; return -1; }\n";
+    o += "            if (!dw_add_stage(v2)) { L.err = kDwFull; return -1; }\n";
     o += "            E" + SI + "(L, top, v2, false, esk, ev, w, o);\n          } else {\n";
     o += "            E" + SI + "(L, top, c.ver, brf, esk, ev, w, o);\n          }\n          break;\n";
   }
@@ -786,7 +797,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "    if (L.err) return -1;\n";
   o += "    if (o.same >= 0) L.set_folds(o.same, w.v, w.nm);\n";
   o += "    if (!(c.stage & kRecEps)) {  // begin state re-added with a new run (NFA.java:148-157)\n";
-  o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = KE_CAPACITY; return -1; }\n";
+  o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = kDwFull; return -1; }\n";
   o += "      if (!L.readd_begin(c.stage & 0xFF, v)) return -1;\n";
   o += "      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
   // Occupancy: at least 3 waves per SIMD (<= 168 VGPRs; measured best: 2 waves lose ~20 %,

@@ -30,12 +30,17 @@
 // the 64 keys of a wavefront are interleaved at 16-B granularity, so lanes touching the
 // same (half, slot, quad) - the common case, the queue loop runs in lockstep - form one
 // fully coalesced 1 KiB access.  A record is kQuads quads: header {stage | Dewey pairs << 24,
-// event, ev_first, Dewey length}, the Dewey (value, count) pairs two per quad (only quads
+// event, ev_first, node hint}, the Dewey (value, count) pairs two per quad (only quads
 // holding live pairs are read or written), then {nullmask, -, fold0, fold1, ...} (64-bit
 // slots) or {nullmask, fold0, fold1, ...} when every fold state is an int (kFold32).
 // A record created at event j does not know the node chain of j until the event ends; it is
 // written with ev_first = kPending and resolved when it is next loaded (event j+1, or the
-// final-match pass of event j itself).
+// final-match pass of event j itself).  Node hint: the buffer node (source stage key, event)
+// of the record, known when the step that made the record put that node (TAKE, BEGIN) or
+// copied from the record it continues (IGNORE).  With deferred walks no node is deleted
+// between two flushes, so put()'s predecessor lookup takes the hint without a memory round
+// trip; a flush clears the hints of the queued records (and walks in place never use them).
+// The Dewey length is not stored: it is the sum of the pair counts.
 //
 // LDS slots (Q::kRingLds = RL > 0).  The first RL slots of each half live in LDS instead of
 // HBM: their header quad, first Dewey quad and fold quads (the quads every record uses); the
@@ -107,11 +112,27 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_WALK_COMPAT2
 #define CEP_WALK_COMPAT2 0
 #endif
+#ifndef CEP_CHAIN_CACHE
+#define CEP_CHAIN_CACHE 0
+#endif
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
 constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
+// a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
+// re-runs the job in the wide one (a retry); the wide build's limit is final
+constexpr int32_t kDwFull = kDeweyPairs < 6 ? KE_RETRY : KE_CAPACITY;
+// Node-chain cache (deferred walks only): the nodes this lane made at the current event and
+// at the previous one, up to kCC each, kept in registers so that put()'s predecessor lookup
+// and the current event's node lookup need no memory round trip.  Exact: every node of an
+// event is made by the key's own lane during that event, nodes are unique per (stage key,
+// event), and with deferred walks nothing deletes a node between two flushes (a flush
+// invalidates the cache; the conflict stamp is still written).  More than kCC nodes at one
+// event: that event's lookups go to memory.
+constexpr int kCC = CEP_CHAIN_CACHE;
+constexpr int kCCs = kCC > 0 ? kCC : 1;
+static_assert(kCC >= 0 && kCC <= 3, "chain cache: 0..3 entries (stage keys packed in 24 bits)");
 
 // may_alias: quads of Node/Pred are also read and written field by field (Node::refs, ...);
 // without it TBAA lets the compiler reorder the two views of the same bytes
@@ -180,6 +201,10 @@ struct Lane {
   uint32_t ochunk = CEP_NONE, opos = 0;
   uint32_t ocur = 0, oend = 0;  // output chunks in hand (kept across the jobs of a persistent lane)
   uint32_t cur_first = CEP_NONE;  // node chain of event j
+  // chain cache (kCC > 0): packed stage keys (byte k) | count << 24 (> kCC: overflow/invalid)
+  uint32_t cc_pack = (kCC + 1u) << 24, pc_pack = (kCC + 1u) << 24;
+  uint32_t cc_id[kCCs], pc_id[kCCs];
+  uint32_t ev_last = CEP_NONE;  // the event of the last event() call (kCC > 0)
   int err = KE_OK;
   uint32_t err_seq = 0;
   uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
@@ -240,8 +265,8 @@ struct Lane {
     r.stage = hd.x & 0x00FFFFFFu;
     r.event = hd.y;
     r.ev_first = hd.z == kPending ? pf : hd.z;
+    r.node = hd.w;
     r.ver.n = hd.x >> 24;
-    r.ver.len = hd.w;
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++) {
       v4u d = {0, 0, 0, 0};
@@ -253,6 +278,11 @@ struct Lane {
         r.ver.c[2 * k + 1] = d.w;
       }
     }
+    uint32_t len = 0;  // DeweyVersion.length(): the digits of every pair
+#pragma unroll
+    for (int k = 0; k < kDeweyPairs; k++)
+      if ((uint32_t)k < r.ver.n) len += r.ver.c[k];
+    r.ver.len = len;
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++) {
@@ -269,9 +299,9 @@ struct Lane {
   }
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
-                                             uint32_t ev_first, const Dewey& ver0) {
+                                             uint32_t ev_first, const Dewey& ver0, uint32_t node) {
     const Dewey ver = dw_pin(ver0);
-    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, ver.len});
+    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, node});
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
@@ -307,14 +337,15 @@ struct Lane {
   // Appends an output record (header + version) and returns its slot, -1 when the queue is
   // full.  ev_first of a record whose event is the current one is only known once the
   // event's nodes exist: kPending, resolved at its next load.  Folds: set_folds.
-  __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver) {
+  __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver,
+                                          uint32_t node = CEP_NONE) {
     if (ocount >= A.rcap) {
       err = KE_RETRY;
       return -1;
     }
     const uint32_t slot = ocount++;
     const uint32_t ef = (event == j && ev_first == CEP_NONE) ? kPending : ev_first;
-    store_head(half ^ 1u, slot, stage, event, ef, ver);
+    store_head(half ^ 1u, slot, stage, event, ef, ver, node);
     if (stage & kRecFinal) n_final++;
     return (int)slot;
   }
@@ -349,6 +380,21 @@ struct Lane {
   }
   __device__ __forceinline__ v4u* PQ(uint32_t p, int k) const { return reinterpret_cast<v4u*>(&PR(p)) + k; }
 
+  // the chain cache's node of stage key sk, CEP_NONE if none (nodes are unique per (sk, event))
+  __device__ __forceinline__ uint32_t cache_find(uint32_t pack, const uint32_t* ids, uint32_t sk) const {
+    uint32_t r = CEP_NONE;
+    const uint32_t n = pack >> 24;
+#pragma unroll
+    for (int k = 0; k < kCC; k++)
+      if ((uint32_t)k < n && ((pack >> (8 * k)) & 0xFFu) == sk) r = ids[k];
+    return r;
+  }
+  __device__ __forceinline__ bool cache_ok(uint32_t pack) const { return kCC > 0 && A.defer && (pack >> 24) <= (uint32_t)kCC; }
+  __device__ __forceinline__ void cache_invalidate() {
+    cc_pack = (kCC + 1u) << 24;
+    pc_pack = (kCC + 1u) << 24;
+  }
+
   // node (sk, event of the chain); CEP_NONE when absent or deleted.  (Pool quads are read as
   // 16-B vectors; v4u is may_alias, so the field writes of the same bytes stay ordered.)
   __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
@@ -374,17 +420,29 @@ struct Lane {
 
   // a new node at event j holding one predecessor (prev, v) in its first-pred slot: both
   // written as whole quads
-  __device__ __forceinline__ void new_node(uint32_t sk, uint32_t prev, const Dewey& v) {
+  __device__ __forceinline__ uint32_t new_node(uint32_t sk, uint32_t prev, const Dewey& v) {
     const uint32_t i = pool_take(A.node_pool, ncur, nend);
     if (i == CEP_NONE) {
       err = KE_RETRY;
-      return;
+      return CEP_NONE;
     }
     const uint32_t p = kPred0 | i;
     write_pred(p, prev, v);
     *NQ(i, 0) = v4u{j, 1u, p, p};
-    *NQ(i, 1) = v4u{cur_first, sk | 0x100u | (1u << 16), 0u, 0u};
+    *NQ(i, 1) = v4u{cur_first, sk | 0x100u | (1u << 16), 0u, key};
     cur_first = i;
+    if (kCC > 0) {
+      const uint32_t n = cc_pack >> 24;
+      if (n < (uint32_t)kCC) {
+#pragma unroll
+        for (int k = 0; k < kCC; k++)
+          if ((uint32_t)k == n) cc_id[k] = i;
+        cc_pack = (cc_pack & ~(0xFFu << (8 * n)) & 0x00FFFFFFu) | (sk << (8 * n)) | ((n + 1) << 24);
+      } else {
+        cc_pack = (kCC + 1u) << 24;  // this event's lookups go to memory
+      }
+    }
+    return i;
   }
 
   // appends (prev, v) to an existing node of event j
@@ -403,12 +461,9 @@ struct Lane {
   }
 
   // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
-  __device__ __forceinline__ void put_begin(uint32_t sk, const Dewey& v) {
-    const uint32_t c = lookup(sk, cur_first);
-    if (c == CEP_NONE) {
-      new_node(sk, CEP_NONE, v);
-      return;
-    }
+  __device__ __forceinline__ uint32_t put_begin(uint32_t sk, const Dewey& v) {
+    const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
+    if (c == CEP_NONE) return new_node(sk, CEP_NONE, v);
     // a new TimedKeyValue with one pointer: the node's first-pred slot, rewritten (the node is
     // of the current event: no queued walk can read its old pointers)
     const uint32_t p = kPred0 | c;
@@ -418,28 +473,43 @@ struct Lane {
     n.head = p;
     n.tail = p;
     n.meta = sk | 0x100u | (1u << 16);
+    return c;
   }
 
-  // put(curr, currEvent, prev, prevEvent, version)  :80-97;  prev_sk == kNoSk: put(begin)
-  __device__ __forceinline__ void put_link(uint32_t sk, uint32_t prev_sk, uint32_t prev_ev, uint32_t prev_first,
-                           const Dewey& v) {
-    if (prev_sk == kNoSk) {
-      put_begin(sk, v);
-      return;
-    }
+  // put(curr, currEvent, prev, prevEvent, version)  :80-97;  prev_sk == kNoSk: put(begin).
+  // (hint_sk, hint): the putting record's node hint; returns the node of (sk, j) (CEP_NONE
+  // on an error)
+  __device__ __forceinline__ uint32_t put_link(uint32_t sk, uint32_t prev_sk, uint32_t prev_ev, uint32_t prev_first,
+                                               const Dewey& v, uint32_t hint_sk = kNoSk, uint32_t hint = CEP_NONE) {
+    if (prev_sk == kNoSk) return put_begin(sk, v);
     if (prev_ev == CEP_NONE) {  // prevEvent.topic on a null Event
       err = KE_NPE;
-      return;
+      return CEP_NONE;
     }
-    const uint32_t p = lookup(prev_sk, prev_first);
+    uint32_t p;
+    if (A.defer && hint != CEP_NONE && prev_sk == hint_sk) p = hint;
+    else if (prev_ev + 1 == j && cache_ok(pc_pack)) p = cache_find(pc_pack, pc_id, prev_sk);
+    else p = lookup(prev_sk, prev_first);
     if (p == CEP_NONE) {  // "Cannot find predecessor event"
       err = KE_ILLEGAL_STATE;
-      return;
+      return CEP_NONE;
     }
     if (A.defer) A.nodes[p].lk = opc;  // found live after `opc` queued walks (conflict check)
-    const uint32_t c = lookup(sk, cur_first);
-    if (c == CEP_NONE) new_node(sk, p, v);
-    else append_pred(c, p, v);
+    const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
+    if (c == CEP_NONE) return new_node(sk, p, v);
+    append_pred(c, p, v);
+    return c;
+  }
+
+  // a flush (walks may delete nodes): the queued records' node hints no longer hold
+  __device__ __forceinline__ void clear_hints() {
+    for (uint32_t i = 0; i < count; i++) {
+      v4u hd = rd(half, i, 0);
+      if (hd.w != CEP_NONE) {
+        hd.w = CEP_NONE;
+        wr(half, i, 0, hd);
+      }
+    }
   }
 
   // TimedKeyValue.getPointerByVersion  TimedKeyValue.java:83-92, from the node's list head:
@@ -603,7 +673,7 @@ struct Lane {
   // A walk step's reads: the node and its first-pred slot, four independent 16-B loads (one
   // memory round trip)
   struct WalkPre {
-    v4u n0, n1, f0, f1;  // {event, refs, head, tail}, {same_next, meta, lk, -}, first pointer quads 0-1
+    v4u n0, n1, f0, f1;  // {event, refs, head, tail}, {same_next, meta, lk, key}, first pointer quads 0-1
   };
   // (both addresses are materialised before the first load: otherwise the compiler computes
   // the second address into registers the first load is still writing and waits for it
@@ -763,6 +833,10 @@ struct Lane {
   // gives each lane one node per iteration, starting its next walk as soon as one ends.
   __device__ __forceinline__ void flush() {
     CEP_STAT(5);
+    if (wq_n) {  // this lane's walks may delete its nodes (no other lane's can)
+      if (kCC > 0) cache_invalidate();
+      clear_hints();
+    }
     const uint32_t id0 = opc - wq_n;
     uint32_t i = 0, s = CEP_NONE, t = 0, flags = 0, np = 0;
     uint64_t npa = 0;
@@ -810,6 +884,13 @@ struct Lane {
     CEP_PT(te0);
     const uint32_t pf = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
+    if (kCC > 0) {  // the last event() call's nodes are the previous event's if it was j - 1
+      pc_pack = ev_last + 1 == j ? cc_pack : (kCC + 1u) << 24;
+#pragma unroll
+      for (int k = 0; k < kCC; k++) pc_id[k] = cc_id[k];
+      cc_pack = 0;
+      ev_last = j;
+    }
     n_final = 0;
     ocount = 0;
     // prefetch the next event's fields (consumed by the next event() call)
@@ -842,6 +923,7 @@ struct Lane {
       b.stage = q.begin_stage;
       b.event = CEP_NONE;
       b.ev_first = CEP_NONE;
+      b.node = CEP_NONE;
       b.nullmask = (1u << F) - 1;
 #pragma unroll
       for (int s = 0; s < F; s++) b.fold[s] = 0;
@@ -1023,6 +1105,10 @@ struct Lane {
     out_first = CEP_NONE;
     wq_n = 0;
     opc = 0;
+    if (kCC > 0) {
+      cache_invalidate();
+      ev_last = CEP_NONE;
+    }
     wt_last = CEP_NONE;
     wm0 = wp0 = 0;
     jj = 0;

@@ -151,8 +151,10 @@ struct QueryRt {
 struct GroupRt {
   std::vector<int> members;
   int F = 2;
-  hipModule_t mod = nullptr;  // JIT tier: the group's kernel (cep_nfa_jit)
+  hipModule_t mod = nullptr;  // JIT tier: the group's kernel (cep_nfa_jit), narrow Dewey build
   hipFunction_t fn = nullptr;
+  hipModule_t mod_wide = nullptr;  // its wide build (compile.cpp generate_jit): re-runs, streams
+  hipFunction_t fn_wide = nullptr;
   hipFunction_t fn_est = nullptr;   // cep_nfa_est (begin stage = one BEGIN edge)
   hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
   double jit_compile_s = 0;
@@ -167,6 +169,7 @@ struct GroupRt {
   cep_batch_stats stats{};  // the last batch
   ~GroupRt() {
     if (mod) (void)hipModuleUnload(mod);
+    if (mod_wide) (void)hipModuleUnload(mod_wide);
     if (sort_tmp) (void)hipFree(sort_tmp);
   }
 };
@@ -340,12 +343,15 @@ void run_stencil(cep_session* s, QueryRt& r) {
   r.ks_dev = r.ks.as<KeyState>();
 }
 
-hipError_t launch_nfa_tier(GroupRt& g, const cep_query* q0, NfaArgs& a, uint64_t nslots, hipStream_t st) {
+// wide: the JIT kernel's wide Dewey build (re-runs, streaming sessions)
+hipError_t launch_nfa_tier(GroupRt& g, const cep_query* q0, NfaArgs& a, uint64_t nslots, hipStream_t st,
+                           bool wide) {
   if (!g.fn) return launch_nfa(g.F, a, nslots, q0->dev.code_len, st);
   if (nslots == 0) return hipSuccess;
   size_t size = sizeof(NfaArgs);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-  return hipModuleLaunchKernel(g.fn, (uint32_t)((nslots + 255) / 256), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return hipModuleLaunchKernel(wide ? g.fn_wide : g.fn, (uint32_t)((nslots + 255) / 256), 1, 1, 256, 1, 1, 0, st,
+                               nullptr, cfg);
 }
 
 hipError_t launch_fn(hipFunction_t fn, NfaArgs& a, uint64_t blocks, hipStream_t st) {
@@ -391,7 +397,12 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // per-lane pool ranges: one atomic per range on each pool's counter.  Per-batch launches
   // (persistent lanes keep their ranges across jobs) take bigger ranges; streams hold a range
   // per key between batches, so theirs stay small
-  const uint32_t nchunk = streaming ? 16 : 64, pchunk = nchunk, ochunk = streaming ? 1 : 8;
+  uint32_t nchunk = streaming ? 16 : 64, ochunk = streaming ? 1 : 8;
+  if (const char* e = std::getenv("CEP_NODE_CHUNK"))  // (measurement runs)
+    if (std::atoi(e) > 0) nchunk = (uint32_t)std::atoi(e);
+  if (const char* e = std::getenv("CEP_OUT_CHUNK"))
+    if (std::atoi(e) > 0) ochunk = (uint32_t)std::atoi(e);
+  const uint32_t pchunk = nchunk;
   const uint64_t ev_q = (uint64_t)((double)s->n_events * (double)Q);
   uint64_t node_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_nodes * 3 / 2 + 4096);
   uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_preds * 3 / 2 + 4096);
@@ -440,6 +451,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
       const uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nn, S.node_cap * 3 / 2), kNodeMax);
       S.nodes.grow_keep(sizeof(Node) * c, sizeof(Node) * S.node_used, s->stream);
       S.preds0.grow_keep(sizeof(Pred) * c, sizeof(Pred) * S.node_used, s->stream);
+      // node slots past the used prefix start dead: pool chunks in hand hold slots no lane
+      // has written yet, which cep_live_floor scans
+      HIPCHECK(hipMemsetAsync(S.nodes.as<Node>() + S.node_used, 0, sizeof(Node) * (c - S.node_used), s->stream));
       S.node_cap = c;
     }
     if (pn > S.pred_cap) {
@@ -521,7 +535,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.prof = s->prof.as<unsigned long long>();
   }
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
-  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream));
+  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
   Scratch h{};
@@ -550,7 +564,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
   g.last_out = h.out_top;
 
   // Re-run the jobs that hit a capacity limit (with 8x the run queue and 4x every exhausted
-  // pool; walks still deferred) and those whose deferred walks conflicted (walks in place).
+  // pool; walks still deferred) and those whose deferred walks conflicted (walks in place),
+  // in the wide Dewey build (a narrow-build job whose version outgrew 3 pairs is a capacity
+  // re-run too).
   // The job lists are collected on the device; only their lengths come back.
   g.stats = cep_batch_stats{};
   g.stats.group_queries = (uint32_t)Q;
@@ -610,7 +626,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
       a.n_jobs = lens[k];
       a.job_next = &sc->job_next;  // re-runs always on persistent lanes
       HIPCHECK(hipMemsetAsync(&sc->job_next, 0, sizeof(uint32_t), s->stream));
-      HIPCHECK(launch_nfa_tier(g, r0.q, a, grid_for(lens[k]), s->stream));
+      HIPCHECK(launch_nfa_tier(g, r0.q, a, grid_for(lens[k]), s->stream, true));
       launches++;
       g.stats.retried_jobs += lens[k];
     }
@@ -719,7 +735,10 @@ const char* cep_query_jit_source(const cep_query* q) { return q ? q->jitSource.c
 int cep_jit_precompile(const cep_query* q, double* compile_s) {
   if (!q) return fail(CEP_E_INVALID, "null query");
   try {
+    double w = 0;
     jit_code_object(q->jitSource, compile_s);
+    jit_code_object(jit_wide_source(q->jitSource), &w);
+    if (compile_s) *compile_s += w;
   } catch (std::exception& e) {
     return fail(CEP_E_COMPILE, e.what());
   }
@@ -736,9 +755,10 @@ int cep_jit_precompile_group(const cep_query* const* queries, int n_queries, dou
   if (compile_s) *compile_s = 0;
   try {
     for (auto& pl : plan_groups(qv)) {
-      double t = 0;
+      double t = 0, w = 0;
       jit_code_object(pl.source, &t);
-      if (compile_s) *compile_s += t;
+      jit_code_object(jit_wide_source(pl.source), &w);
+      if (compile_s) *compile_s += t + w;
     }
   } catch (std::exception& e) {
     return fail(CEP_E_COMPILE, e.what());
@@ -844,6 +864,11 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         std::vector<char> co = jit_code_object(pl.source, &g->jit_compile_s);
         HIPCHECK(hipModuleLoadData(&g->mod, co.data()));
         HIPCHECK(hipModuleGetFunction(&g->fn, g->mod, "cep_nfa_jit"));
+        double w = 0;
+        std::vector<char> cw = jit_code_object(jit_wide_source(pl.source), &w);
+        g->jit_compile_s += w;
+        HIPCHECK(hipModuleLoadData(&g->mod_wide, cw.data()));
+        HIPCHECK(hipModuleGetFunction(&g->fn_wide, g->mod_wide, "cep_nfa_jit"));
         if (pl.source.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
           HIPCHECK(hipModuleGetFunction(&g->fn_est, g->mod, "cep_nfa_est"));
           HIPCHECK(hipModuleGetFunction(&g->fn_bits, g->mod, "cep_nfa_bits"));
@@ -873,6 +898,7 @@ int cep_session_reset(cep_session* s) {
       // slots are rewritten from scratch); empty pools
       HIPCHECK(hipMemsetAsync(S.carry.p, 0, sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1), s->stream));
       HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
+      if (S.node_used) HIPCHECK(hipMemsetAsync(S.nodes.p, 0, sizeof(Node) * S.node_used, s->stream));
       S.node_used = S.pred_used = 0;
     }
     s->watermark = INT64_MIN;
@@ -1243,6 +1269,26 @@ int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size) {
       d2h(S.preds0.p, sizeof(Pred) * S.node_used);
       d2h(S.preds.p, sizeof(Pred) * S.pred_used);
     }
+  });
+}
+
+int cep_live_floor(cep_session* s, int query, uint32_t* floor, uint64_t n_keys) {
+  if (!s || !floor || query < 0 || query >= (int)s->qs.size()) return fail(CEP_E_INVALID, "bad argument");
+  if (!s->opts.streaming) return fail(CEP_E_STATE, "cep_live_floor needs a streaming session (cep_opts.streaming)");
+  QueryRt& r = *s->qs[query];
+  const StreamState& S = r.st;
+  if (S.init && n_keys > S.n_keys) return fail(CEP_E_INVALID, "n_keys larger than the session's key space");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    if (!S.init || n_keys == 0) {
+      for (uint64_t k = 0; k < n_keys; k++) floor[k] = 0xFFFFFFFFu;
+      return;
+    }
+    DBuf out;
+    out.ensure(4 * S.n_keys);
+    HIPCHECK(launch_live_floor(S.nodes.as<Node>(), S.node_used, S.n_keys, out.as<uint32_t>(), s->stream));
+    HIPCHECK(hipMemcpyAsync(floor, out.p, 4 * n_keys, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
   });
 }
 

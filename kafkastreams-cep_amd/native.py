@@ -25,7 +25,7 @@ EXPORTS = [
     "cep_session_create", "cep_session_destroy", "cep_push_batch", "cep_sync", "cep_poll_matches",
     "cep_key_errors", "cep_match_digest", "cep_watermark", "cep_last_timing", "cep_last_error",
     "cep_alloc_pinned", "cep_free_pinned", "cep_device_alloc", "cep_device_free", "cep_memcpy",
-    "cep_query_jit_source", "cep_jit_precompile", "cep_session_reset",
+    "cep_query_jit_source", "cep_jit_precompile", "cep_session_reset", "cep_live_floor",
     "cep_batch_layout", "cep_session_snapshot", "cep_session_restore",
     "cep_decode_stock_json", "cep_jit_precompile_group", "cep_query_group_plan",
     "cep_last_stats", "cep_gather_keys", "cep_timing_totals", "cep_symbol_keys", "cep_lane_balance",
@@ -111,6 +111,7 @@ def lib():
             "cep_session_snapshot": ([vp, vp, C.c_size_t, C.POINTER(C.c_size_t)], C.c_int),
             "cep_session_restore": ([vp, vp, C.c_size_t], C.c_int),
             "cep_session_reset": ([vp], C.c_int),
+            "cep_live_floor": ([vp, C.c_int, C.POINTER(u32), u64], C.c_int),
             "cep_decode_stock_json": ([C.c_int, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp], C.c_int),
             "cep_symbol_keys": ([C.c_int, vp, vp, vp, vp, u64, u64, vp, C.POINTER(u64), vp], C.c_int),
             "cep_lane_balance": ([vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
@@ -600,6 +601,14 @@ class Session:
         st = BatchStats()
         _check(lib().cep_last_stats(self.h, query, C.byref(st)))
         return {k: getattr(st, k) for k, _ in BatchStats._fields_}
+
+    def live_floor(self, query: int = 0, n_keys: int | None = None) -> np.ndarray:
+        """cep_live_floor: per key, the oldest sequence number a live buffer node still holds
+        (0xFFFFFFFF: none) - a streaming session's only events a later match can contain."""
+        n = self.n_keys if n_keys is None else n_keys
+        out = np.zeros(n, np.uint32)
+        _check(lib().cep_live_floor(self.h, query, out.ctypes.data_as(C.POINTER(C.c_uint32)), n))
+        return out
 
     def reset(self) -> None:
         """cep_session_reset: every key of a streaming session back to the NFA's initial

@@ -23,11 +23,32 @@ partition (CEPProcessor.java:117-134), so records of different keys share runs; 
 processor keeps one NFA per key (a Kafka partition is usually one key's stream in the
 reference's demo, where both give the same matches).
 
-The processor keeps every record it was given (the `Event`s a later match may reference) in
-host memory; `max_keys` bounds the dense key space of the device session.  There is no CPU
-matching path: without libcep.so and a GPU, `init()` raises.
+State.  The device session holds every key's NFA (run queue, shared buffer, folds).  The host
+keeps, per key, only the records a later match can still contain: after each flush the
+session reports, per key, the oldest event a live buffer node holds (`cep_live_floor`) and
+older records are dropped - the same events the reference's buffer store still holds
+(KVSharedVersionedBuffer.java:143-171 deletes a node once its last reference is walked).  A
+query whose runs never die (the README query: WITHIN never prunes in the reference, SURVEY
+§0.3) pins its runs' events there as it does in the reference's store.  `max_keys` bounds the
+dense key space of the device session.
+
+Persistence (`in_memory=False`, the reference's default, CEPProcessor.java:71-84,144-149).  The
+reference writes the NFA's run queue to the `_cep_nfa` store after every record (:159-160) and
+reloads it in `init` (:117-134).  Here the processor's whole state - the device session's
+snapshot (`cep_session_snapshot`: run queues, buffers, folds, Dewey versions, sequence
+numbers of every key) and the retained records - is written to the `_cep_nfa` store, keyed by
+(topic, partition) as the reference keys it, at every commit (`punctuate`, `close`), and
+reloaded in `init`.  Records processed after the last commit are replayed by the host after a
+restart (Kafka's at-least-once delivery), so a processor recreated from the store forwards
+exactly what one uninterrupted processor would.  The store is whatever `context.get_state_store
+("_cep_nfa")` returns (any mutable mapping; a real host passes its persistent store), or the
+`store` argument.
+
+There is no CPU matching path: without libcep.so and a GPU, `init()` raises.
 """
 from __future__ import annotations
+
+import pickle
 
 import numpy as np
 
@@ -65,6 +86,9 @@ class CapacityError(JavaException):
 
 
 _EXC = {1: NullPointerException, 2: IllegalStateException, 3: ArithmeticException, 16: CapacityError}
+
+NFA_STATES_STORE = "_cep_nfa"  # CEPProcessor.java:56
+_CKPT_MAGIC = b"CEPPROC1"
 
 
 # ---- Event / Sequence ---------------------------------------------------------------------
@@ -146,8 +170,12 @@ class RecordContext:
     timestamp)` plays a record into a processor the way a stream task does (offsets count up
     per topic partition).  A real host passes its own context with the same members."""
 
-    def __init__(self, topic: str = "topic", partition: int = 0):
+    def __init__(self, topic: str = "topic", partition: int = 0, stores: dict | None = None):
+        """stores: name -> mutable mapping, the context's state stores (Kafka's
+        ProcessorContext.getStateStore); pass the same dict to a new context to play a restart
+        from persistent stores."""
         self._topic, self._partition = topic, partition
+        self.stores = {} if stores is None else stores
         self._offset, self._timestamp = -1, 0
         self.forwarded: list = []
         self.processor = None
@@ -167,6 +195,12 @@ class RecordContext:
     def forward(self, key, value):
         self.forwarded.append((key, value))
 
+    def get_state_store(self, name: str):
+        """ProcessorContext.getStateStore: the store of that name (created empty on first use)"""
+        return self.stores.setdefault(name, {})
+
+    getStateStore = get_state_store
+
     def send(self, key, value, timestamp: int, offset: int | None = None):
         self._offset = self._offset + 1 if offset is None else int(offset)
         self._timestamp = int(timestamp)
@@ -178,12 +212,16 @@ class CEPProcessor:
     """CEPProcessor.java:54-193 over a streaming libcep session (one NFA per key)."""
 
     def __init__(self, pattern, in_memory: bool = False, *, batch_size: int = 4096,
-                 max_keys: int = 1 << 16, device: int = 0, session_factory=None, semantic_within: bool = False):
+                 max_keys: int = 1 << 16, device: int = 0, session_factory=None, semantic_within: bool = False,
+                 store=None):
         """semantic_within: enforce the query's WITHIN on the record timestamps (this build's
         semantic mode, Pattern.to_ir(semantic_within=True)); the default is the reference's
-        behaviour, where WITHIN never prunes."""
+        behaviour, where WITHIN never prunes.  in_memory=False (the reference's default): the
+        state is checkpointed to the `_cep_nfa` store at every commit and reloaded by init();
+        `store` overrides the context's store."""
         self.pattern = pattern
-        self.in_memory = in_memory  # the reference's store choice; device state is in HBM either way
+        self.in_memory = in_memory  # the reference's store choice (CEPProcessor.java:144-149)
+        self._store = store
         self.batch_size = max(1, int(batch_size))
         self.max_keys = int(max_keys)
         self.device = device
@@ -197,7 +235,11 @@ class CEPProcessor:
         self.query = None
         self._key_ids: dict = {}
         self._keys: list = []
-        self._events: list[list[Event]] = []  # per key id, in arrival order (sequence number)
+        # per key id: the records a later match can still contain, in arrival order; record i of
+        # the list has sequence number _ev_base[k] + i; _ev_total[k] records were given so far
+        self._events: list[list[Event]] = []
+        self._ev_base: list[int] = []
+        self._ev_total: list[int] = []
         self._buf_key: list[int] = []
         self._buf_vals: list[tuple] = []
         self._buf_ts: list[int] = []
@@ -216,6 +258,53 @@ class CEPProcessor:
             self.query = N.Query(self.ir)
             self.session = N.Session(self.query, device=self.device, streaming=True)
         self.stage_names = list(getattr(self.session, "stage_names", None) or self.query.stage_names)
+        store = self._state_store()
+        if store is not None:  # initializeIfNotAndGet :121-131: the NFA as the store holds it
+            blob = store.get(self._store_key())
+            if blob is not None:
+                self.restore(blob)
+
+    # -- persistence (in_memory=False) --
+    def _state_store(self):
+        if self.in_memory:
+            return None
+        if self._store is not None:
+            return self._store
+        get = getattr(self.context, "get_state_store", None) or getattr(self.context, "getStateStore", None)
+        return get(NFA_STATES_STORE) if get is not None else None
+
+    def _store_key(self):
+        """TopicAndPartition(context.topic(), context.partition()) (CEPProcessor.java:121-122)"""
+        return (self.context.topic(), self.context.partition())
+
+    def checkpoint(self) -> bytes:
+        """The processor's whole state as one blob: the device session's snapshot (every key's
+        NFA) and the retained records with their per-key sequence numbers."""
+        dev = self.session.snapshot()
+        host = pickle.dumps({"keys": self._keys, "events": self._events, "base": self._ev_base,
+                             "total": self._ev_total, "max_keys": self.max_keys, "ir": self.ir},
+                            protocol=pickle.HIGHEST_PROTOCOL)
+        return _CKPT_MAGIC + len(dev).to_bytes(8, "little") + dev + host
+
+    def restore(self, blob: bytes) -> None:
+        """Loads a checkpoint() blob written by a processor over the same pattern (the
+        processor's own store data; never a file from elsewhere)."""
+        if blob[:8] != _CKPT_MAGIC:
+            raise ValueError("not a CEPProcessor checkpoint")
+        n = int.from_bytes(blob[8:16], "little")
+        host = pickle.loads(blob[16 + n:])
+        if host["ir"] != self.ir or host["max_keys"] != self.max_keys:
+            raise ValueError("checkpoint of another pattern or key space")
+        self.session.restore(blob[16:16 + n])
+        self._keys = list(host["keys"])
+        self._key_ids = {k: i for i, k in enumerate(self._keys)}
+        self._events, self._ev_base, self._ev_total = host["events"], host["base"], host["total"]
+
+    def commit(self) -> None:
+        """Writes the checkpoint into the `_cep_nfa` store (a no-op in memory)."""
+        store = self._state_store()
+        if store is not None and self._failed is None:
+            store[self._store_key()] = self.checkpoint()
 
     def process(self, key, value) -> None:
         """CEPProcessor.java:155-163."""
@@ -230,9 +319,12 @@ class CEPProcessor:
             kid = self._key_ids[key] = len(self._keys)
             self._keys.append(key)
             self._events.append([])
+            self._ev_base.append(0)
+            self._ev_total.append(0)
         ctx = self.context
         ev = Event(key, value, ctx.timestamp(), ctx.topic(), ctx.partition(), ctx.offset())
         self._events[kid].append(ev)
+        self._ev_total[kid] += 1
         self._buf_key.append(kid)
         self._buf_vals.append(self._columns_of(value))
         self._buf_ts.append(ev.timestamp)
@@ -240,14 +332,17 @@ class CEPProcessor:
             self.flush()
 
     def punctuate(self, timestamp: int) -> None:
-        """CEPProcessor.java:167-169 (empty there): forwards what is buffered."""
+        """CEPProcessor.java:167-169 (empty there): forwards what is buffered, then commits
+        the state to the `_cep_nfa` store (in_memory=False)."""
         self.flush()
+        self.commit()
 
     def close(self) -> None:
-        """CEPProcessor.java:172-175: forwards what is buffered and frees the session."""
+        """CEPProcessor.java:172-175: forwards what is buffered, commits, frees the session."""
         try:
             if self.session is not None and self._failed is None:
                 self.flush()
+                self.commit()
         finally:
             if self.session is not None and hasattr(self.session, "close"):
                 self.session.close()
@@ -277,15 +372,22 @@ class CEPProcessor:
         # per key: the sequence number of its first record in this batch, and the arrival
         # index of each of its records (a stable partition of the batch by key)
         counts = np.bincount(keys, minlength=len(self._keys)).astype(np.int64)
-        total = np.asarray([len(e) for e in self._events], np.int64)
+        total = np.asarray(self._ev_total, np.int64)
         before = total - counts
+        base = np.asarray(self._ev_base, np.int64)
         by_key = np.argsort(keys, kind="stable")
         start = np.zeros(len(self._keys) + 1, np.int64)
         np.cumsum(counts, out=start[1:])
 
-        self.session.push_arrival(keys, cols, self.max_keys, ts)
-        m = self.session.matches(0)
-        code, err_seq = self.session.key_errors(0, self.max_keys)
+        try:
+            self.session.push_arrival(keys, cols, self.max_keys, ts)
+            m = self.session.matches(0)
+            code, err_seq = self.session.key_errors(0, self.max_keys)
+        except N.CepError as e:
+            # the records are consumed (appended above) but the device state is unknown: the
+            # processor cannot continue consistently
+            self._failed = JavaException(f"libcep failed on a batch of {n} records: {e}")
+            raise self._failed from e
 
         def arrival(k, seq):
             return by_key[start[k] + (np.asarray(seq, np.int64) - before[k])]
@@ -314,16 +416,34 @@ class CEPProcessor:
             for i in order.tolist():
                 if emit[i] >= fail_at:
                     break
-                evs = self._events[mk[i]]
+                evs, b0 = self._events[mk[i]], base[mk[i]]
                 seq = Sequence()
                 for p in range(off[i], off[i + 1]):
-                    seq.add(names[pst[p]], evs[pseq[p]])
+                    seq.add(names[pst[p]], evs[pseq[p] - b0])
                 fwd(None, seq)
         if fail_key >= 0:
             c = int(code[fail_key])
-            ev = self._events[fail_key][int(err_seq[fail_key])]
+            ev = self._events[fail_key][int(err_seq[fail_key]) - int(base[fail_key])]
             exc = _EXC.get(c, JavaException)
             self._failed = exc(f"{exc.__name__} in the NFA of key {self._keys[fail_key]!r} at "
                                f"offset {ev.offset} (cep_key_errors code {c})",
                                key=self._keys[fail_key], event=ev)
             raise self._failed
+        self._drop_unreachable(np.flatnonzero(counts))
+
+    def _drop_unreachable(self, touched) -> None:
+        """Drops the records of the batch's keys that no live buffer node holds any more
+        (cep_live_floor): no later match can contain them."""
+        if len(touched) == 0 or not hasattr(self.session, "live_floor"):
+            return
+        floor = self.session.live_floor(0, len(self._keys))
+        for k in touched.tolist():
+            keep = min(int(floor[k]), self._ev_total[k])
+            cut = keep - self._ev_base[k]
+            if cut > 0:
+                del self._events[k][:cut]
+                self._ev_base[k] = keep
+
+    def retained_records(self) -> int:
+        """records held on the host (the ones a later match can still contain)"""
+        return sum(len(e) for e in self._events)

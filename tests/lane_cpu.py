@@ -25,11 +25,14 @@ BUILD = os.path.join(os.environ.get("TMPDIR", "/tmp"), "cep_lane_cpu")
 _libs = {}
 
 
-def build(ir: bytes, source: str | None = None):
+def build(ir: bytes, source: str | None = None, narrow: bool = False):
     """Compile the query's kernel (or a group's `source`) for the host; returns the loaded
-    library (cached)."""
+    library (cached).  The wide Dewey build (6 pairs) unless `narrow`: the driver re-runs jobs
+    in the same build, while libcep re-runs the narrow build's overflowing jobs in the wide one."""
     # the occupancy attribute is for the GPU compile only (the host has no kernels)
     src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\d+\)\)\)", "", source or N.Query(ir).jit_source)
+    if not narrow:
+        src = "#define CEP_DEWEY_PAIRS 6\n" + src
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
                    ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
@@ -60,11 +63,12 @@ def build(ir: bytes, source: str | None = None):
     return lib
 
 
-def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None, ts=None):
+def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None, ts=None,
+        narrow=False):
     """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
     the batch continues the keys' streams of the previous streaming call (reset=False).
     bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the chunked scan."""
-    lib = build(ir, _group["source"] if _group else None)
+    lib = build(ir, _group["source"] if _group else None, narrow=narrow)
     n_q = len(_group["members"]) if _group else 1
     kc = np.ascontiguousarray(_group["literals"], np.int64) if _group else None
     if streaming and reset:

@@ -174,7 +174,8 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       if (ks[k].err == KE_RETRY || ks[k].err == KE_CONFLICT) list.push_back((uint32_t)k);
     *n_retried += (uint32_t)list.size();
     n_cap = 0;
-    rcap *= 8;
+    // (session.cpp keeps the re-run rings within 16 GiB; here 2 GiB)
+    if ((uint64_t)rcap * 8 * ((list.size() + 63) / 64 * 64) * 192 <= (2ull << 30)) rcap *= 8;
     std::vector<uint32_t> cap, conf;  // session.cpp: capacity re-runs keep deferred walks, conflicts walk in place
     for (uint32_t k : list) (ks[k].err == KE_RETRY ? cap : conf).push_back(k);
     for (int k = 0; k < 2; k++) {

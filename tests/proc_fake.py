@@ -63,6 +63,14 @@ class OracleStreamSession:
                 seq[k] = int(r["err_pos"][j]) - int(off[j])
         self._err = (code, seq)
 
+    def snapshot(self) -> bytes:
+        import pickle  # (this fake's own state)
+        return pickle.dumps(self.hist)
+
+    def restore(self, blob: bytes) -> None:
+        import pickle
+        self.hist = pickle.loads(blob)
+
     def matches(self, query=0):
         return self._m
 

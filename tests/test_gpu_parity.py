@@ -115,6 +115,21 @@ def test_stencil_key_boundaries(m, chain):
     assert_parity(gpu_run(ir, off, [v]), r, off)
 
 
+def test_stencil_empty_batch_after_matches():
+    """an empty batch on a session whose previous stencil batch matched reports no
+    matches and checksum 0 (not the previous batch's pinned count)."""
+    q = N.Query(W.strict_abc_query().to_ir())
+    s = N.Session(q)
+    off, cols = W.generate(W.SynthConfig("t", "abc", 100, 300, 0xCE90000 + 2))
+    s.push(off, cols)
+    assert s.digest(0)[0] > 0
+    s.push(np.zeros(101, np.uint64), [np.zeros(0, np.int32)])
+    assert s.digest(0) == (0, 0)
+    assert s.matches(0)["n_matches"] == 0
+    s.push(off, cols)  # and the session still works
+    assert_parity(session_result(s, 0, off, q.kind), oracle.run(q.ir, off, cols), off)
+
+
 def test_stencil_pipelined_pushes():
     """Stencil pushes return without a host sync: batches queued back to back, then the last
     batch's results, and the device time of every batch (cep_timing_totals)."""
@@ -151,6 +166,20 @@ def test_cfg4_any_kleene_small(tier):
     off, cols = W.generate(cfg)
     ir = W.any_kleene_query().to_ir()
     assert_parity(gpu_run(ir, off, cols, tier=tier), oracle.run(ir, off, cols, threads=8), off)
+
+
+@pytest.mark.parametrize("tier", TIERS)
+def test_cfg4_stress_variant_small(tier):
+    """Config 4's benched stress variant (S1 carries volume, S2 reads it with getOrElse): no
+    key throws, runs accumulate, bit-exact against the oracle on 500 keys
+    of the cfg-3 stream."""
+    cfg = W.CONFIGS[3]
+    keys = np.arange(0, 1_000_000, 2000)[:500]
+    off, cols = W.generate(cfg, keys)
+    ir = W.any_kleene_query(carry_volume=True).to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    assert r["n_matches"] > 100 and int(np.count_nonzero(r["err_code"])) == 0
+    assert_parity(gpu_run(ir, off, cols, tier=tier), r, off)
 
 
 @pytest.mark.parametrize("groups", [True, False])
@@ -440,6 +469,48 @@ def test_streaming_snapshot_restore(query):
         s.restore(blob)
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
     np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
+def test_streaming_reset_restarts_every_key():
+    """cep_session_reset: a streaming session that has run batches and is reset matches a
+    fresh session pushed the same batches (allocations reused, every key from the initial
+    state)."""
+    import stream_split as SS
+    cfg = W.SynthConfig("t", "stock", 300, 600, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    s = N.Session(N.Query(ir), streaming=True)
+    parts = SS.split(off, cols, 3, seed=3)
+    for ko, cs in parts[:2]:
+        s.push(ko, cs)
+    s.reset()
+    outs = []
+    for ko, cs in parts:
+        s.push(ko, cs)
+        outs.append(s.matches(0))
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    assert s.watermark() == np.iinfo(np.int64).min
+
+
+def test_streaming_device_slices_checksum():
+    """bench.py's streaming figure: the stream cut per key into consecutive device slices
+    (native.gather_ranges) and pushed through one streaming session gives, summed over the
+    batches, the per-batch session's match count and checksum of the whole stream."""
+    import bench
+    cfg = W.CONFIGS[3]
+    stream = N.synth_stream("stock", cfg.seed, 3000, 1000)
+    q = N.Query(W.stock_query("readme").to_ir())
+    whole = N.Session(q)
+    whole.push_device(stream)
+    want = whole.digest(0)
+    s = N.Session(q, streaming=True)
+    n, dig = 0, 0
+    for p in bench.slice_stream(stream, 7):
+        s.push_device(p)
+        m, d = s.digest(0)
+        n, dig = n + m, (dig + d) % (1 << 64)
+    assert want[0] > 100 and (n, dig) == want
 
 
 def test_snapshot_rejects_mismatch():

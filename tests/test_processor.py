@@ -211,7 +211,109 @@ def test_key_exception_after_earlier_matches_cpu(batch):
     _check_error_run(False, batch)
 
 
+def _check_restart_from_store(gpu, batch, commit_every, crash_at):
+    """in_memory=False: the processor commits its state to the `_cep_nfa` store on punctuate;
+    after a crash a new processor (same stores) restores it in init(), the records since the
+    last commit are replayed (Kafka's at-least-once delivery), and the Sequences forwarded
+    after the restart complete exactly the uninterrupted run's (CEPProcessor.java:117-134,
+    159-160)."""
+    recs = random_records(13, n_keys=40 if gpu else 8, n=1500 if gpu else 240)
+    q = W.stock_query("readme")
+    exp, emit, err = expected_view(q, recs)
+    assert not err and len(exp) > 5
+    stores = {}
+    ctx = P.RecordContext("StockEvents", 3, stores=stores)
+    proc = P.CEPProcessor(q, batch_size=batch, max_keys=256, session_factory=_factory(gpu))
+    proc.init(ctx)
+    committed, n_fwd_at_commit = 0, 0
+    for i, (k, v, ts) in enumerate(recs[:crash_at]):
+        ctx.send(k, v, ts, offset=i)
+        if (i + 1) % commit_every == 0:
+            proc.punctuate(ts)
+            committed, n_fwd_at_commit = i + 1, len(ctx.forwarded)
+    assert P.NFA_STATES_STORE in stores and ("StockEvents", 3) in stores[P.NFA_STATES_STORE]
+    before = forwarded_view(ctx)[:n_fwd_at_commit]
+    # crash: the processor and its device session are gone (nothing after the commit survives)
+    if hasattr(proc.session, "close"):
+        proc.session.close()
+    ctx2 = P.RecordContext("StockEvents", 3, stores=stores)
+    proc2 = P.CEPProcessor(q, batch_size=batch, max_keys=256, session_factory=_factory(gpu))
+    proc2.init(ctx2)
+    for i, (k, v, ts) in enumerate(recs[committed:], start=committed):
+        ctx2.send(k, v, ts, offset=i)
+    proc2.close()
+    assert before + forwarded_view(ctx2) == exp
+
+
+@pytest.mark.parametrize("batch,commit_every,crash_at", [(4, 50, 130), (64, 37, 200), (1, 100, 100)])
+def test_restart_from_store_cpu(batch, commit_every, crash_at):
+    _check_restart_from_store(False, batch, commit_every, crash_at)
+
+
+def test_in_memory_writes_no_store():
+    stores = {}
+    ctx = P.RecordContext("t", 0, stores=stores)
+    proc = P.CEPProcessor(W.stock_query("readme"), in_memory=True, batch_size=4, session_factory=OracleStreamSession)
+    proc.init(ctx)
+    for k, v, ts in _readme_records():
+        ctx.send(k, v, ts)
+    proc.close()
+    assert stores == {}
+
+
 # ---- through libcep on the GPU -----------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,commit_every,crash_at", [(16, 200, 700), (1000, 500, 1200)])
+def test_restart_from_store_gpu(batch, commit_every, crash_at):
+    _check_restart_from_store(True, batch, commit_every, crash_at)
+
+
+@pytest.mark.gpu
+def test_retained_records_bounded_gpu():
+    """1e6 records over 500 keys through the strict SEQ(A, B, C) query (runs die within three
+    records, their nodes are deleted by removePattern / match extraction): the records the
+    processor holds stay bounded (cep_live_floor), and the forwarded matches equal the
+    oracle's.  Bound: a key's live nodes span its last two records; plus one batch."""
+    rng = np.random.default_rng(3)
+    n, n_keys, batch = 1_000_000, 500, 20_000
+    keys = rng.integers(0, n_keys, size=n)
+    vals = rng.integers(0, 16, size=n).astype(np.int32)
+    q = W.strict_abc_query()
+    ctx = P.RecordContext("t", 0)
+    proc = P.CEPProcessor(q, batch_size=batch, max_keys=n_keys)
+    proc.init(ctx)
+    most = 0
+    n_fwd = 0
+    for i in range(n):
+        ctx.send(int(keys[i]), {"v": int(vals[i])}, T0 + i)
+        if (i + 1) % batch == 0:
+            most = max(most, proc.retained_records())
+            n_fwd += len(ctx.forwarded)
+            ctx.forwarded.clear()
+    proc.close()
+    n_fwd += len(ctx.forwarded)
+    assert most <= 3 * n_keys, most
+    off = np.zeros(n_keys + 1, np.uint64)
+    np.cumsum(np.bincount(keys, minlength=n_keys), out=off[1:])
+    r = oracle.run(q.to_ir(), off, [vals[np.argsort(keys, kind="stable")]])
+    assert n_fwd == r["n_matches"] > 1000
+
+
+@pytest.mark.gpu
+def test_live_floor_stock_query_gpu():
+    """cep_live_floor on the README query: every key's floor is at most the first record of a
+    live run's chain; records before a key's first begin event (volume > 1000) are dropped."""
+    recs = random_records(17, n_keys=30, n=3000)
+    ctx = P.RecordContext("StockEvents", 0)
+    proc = P.CEPProcessor(W.stock_query("readme"), batch_size=500, max_keys=64)
+    proc.init(ctx)
+    for k, v, ts in recs:
+        ctx.send(k, v, ts)
+    proc.flush()
+    assert proc.retained_records() < len(recs)
+    exp, _, _ = expected_view(W.stock_query("readme"), recs)
+    assert forwarded_view(ctx) == exp
+    proc.close()
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", [1, 3, 1000])
 def test_readme_demo_gpu(batch):

@@ -82,6 +82,12 @@ def test_gpu_symbol_keys_many_symbols_and_small_table():
     np.testing.assert_array_equal(keys.download(np.uint32, len(recs)), np.array(want, np.uint32))
     with pytest.raises(N.CepError):  # more names than the table holds
         N.symbol_keys(b, d, max_symbols=100)
+    # between n_sym/2 and n_sym the table (>= 2 x max_symbols slots) does not fill,
+    # but the limit still fails the call
+    for m in (2600, 4000, 4999):
+        with pytest.raises(N.CepError):
+            N.symbol_keys(b, d, max_symbols=m)
+    assert N.symbol_keys(b, d, max_symbols=5000)[1] == 5000
 
 
 @pytest.mark.gpu
