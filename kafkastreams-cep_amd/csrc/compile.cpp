@@ -840,6 +840,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "      w += n - (uint32_t)(s + b - base);\n    }\n  }\n";
     o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
+    o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
     // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
     // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).

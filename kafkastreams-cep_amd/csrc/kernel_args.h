@@ -53,6 +53,8 @@ struct NfaArgs {
                              // throws at CSR position p (quiet lanes jump to the next set bit)
   uint64_t n_events;         // CSR positions of the batch (bits kernel)
   uint32_t* n_capacity_err;  // jobs to re-run (KE_RETRY / KE_CONFLICT)
+  uint32_t* full;            // bit 0: a run queue overflowed this launch (the next batch starts
+                             // with a bigger one, session.cpp)
   unsigned long long* prof;  // measurement builds ($CEP_PROF): the time split of nfa_lane.h, 16 counters
 };
 

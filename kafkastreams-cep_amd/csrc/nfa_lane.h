@@ -341,6 +341,7 @@ struct Lane {
                                           uint32_t node = CEP_NONE) {
     if (ocount >= A.rcap) {
       err = KE_RETRY;
+      if (A.full) atomicOr(A.full, 1u);
       return -1;
     }
     const uint32_t slot = ocount++;
@@ -1270,8 +1271,11 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   Lane<F, Q> L(A, q);
   L.key = key;
   L.n_ev = (uint32_t)(A.key_off[key + 1] - A.key_off[key]);
+  // a stream's run queue lives at its key's position (kept from batch to batch whatever lane
+  // order the batch runs in); a per-batch launch's at the lane's slot (coalesced)
+  const uint64_t rslot = A.carry ? job : slot;
   L.rb = reinterpret_cast<v4u*>(A.rings) +
-         (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (slot % 64);
+         (rslot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (rslot % 64);
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);

@@ -81,7 +81,7 @@ template <class T> struct HVec {  // host copy of a result array
 struct Scratch {  // small counters, one allocation
   uint32_t node_top, pred_top, out_top, n_cap_err;
   uint32_t tile_counter, overflow, n_retry_cap, n_retry_conflict;
-  uint32_t job_next, pad2;
+  uint32_t job_next, full;  // full: NfaArgs.full
   uint64_t totals[2];
   uint64_t total;
   unsigned long long digest;
@@ -166,6 +166,7 @@ struct GroupRt {
   size_t sort_tmp_bytes = 0;
   // pool use of the last batch (the next batch's pools are sized from it)
   uint64_t last_nodes = 0, last_preds = 0, last_out = 0;
+  uint32_t rcap_hint = 0;  // run-queue slots per key: grown when a batch's queues overflowed
   cep_batch_stats stats{};  // the last batch
   ~GroupRt() {
     if (mod) (void)hipModuleUnload(mod);
@@ -372,6 +373,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   const uint64_t jobs = Q * nk;
   QueryRt& r0 = *s->qs[g.members[0]];
   uint32_t rcap = s->opts.max_runs ? s->opts.max_runs : 32;
+  const bool streaming0 = s->opts.streaming != 0;
+  if (!streaming0) rcap = std::max(rcap, g.rcap_hint);  // (a stream's ring geometry is fixed)
   const double pf = s->opts.pool_factor > 0 ? s->opts.pool_factor : 0.0625;
   const bool streaming = s->opts.streaming != 0;  // (a streaming group holds one query)
   // Per-batch sessions run persistent lanes (nfa_lane.h run_jobs): a grid of about what the
@@ -486,6 +489,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.out_pool = Pool{&sc->out_top, (uint32_t)out_cap, ochunk};
   a.ks = g.ks.as<KeyState>();
   a.n_capacity_err = &sc->n_cap_err;
+  a.full = &sc->full;
   a.n_events = s->n_events;
   if (persist) {
     a.job_next = &sc->job_next;
@@ -513,8 +517,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
   }
   // Lane order: keys sorted by estimated work, longest first (cep_nfa_est, from the begin-hit bitmap), so a wave's 64
   // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
-  // start first.  Streams keep the identity order (their run queues live at the key's slot).
-  if (g.fn_est && !streaming && nk > 64) {
+  // start first.  (A stream's run queues live at the key's position, so its lanes too may run
+  // in any order; its estimate adds the runs each key carries.)
+  if (g.fn_est && nk > 64) {
     g.est.ensure(4 * nk);
     g.est_sorted.ensure(4 * nk);
     g.order.ensure(4 * nk);
@@ -562,6 +567,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
   g.last_nodes = h.node_top;
   g.last_preds = h.pred_top;
   g.last_out = h.out_top;
+  // a run queue overflowed: its jobs are re-run below, and the next batch starts with 4x the
+  // slots (run queues past the LDS slots live in HBM: a bigger ring costs memory, not time),
+  // the ring kept within 32 GiB
+  if (!streaming && (h.full & 1u)) {
+    uint32_t nr = rcap * 4;
+    while (nr > rcap && ring_size(g.F, std::max<uint64_t>(slots, 1), nr) > (32ull << 30)) nr /= 2;
+    g.rcap_hint = nr;
+  }
 
   // Re-run the jobs that hit a capacity limit (with 8x the run queue and 4x every exhausted
   // pool; walks still deferred) and those whose deferred walks conflicted (walks in place),

@@ -25,6 +25,11 @@ inline unsigned atomicAdd(unsigned* p, unsigned v) {
   *p += v;
   return o;
 }
+inline unsigned atomicOr(unsigned* p, unsigned v) {
+  const unsigned o = *p;
+  *p = o | v;
+  return o;
+}
 inline bool __any(int x) { return x != 0; }  // a wave of one lane
 // a wave of one lane: the calling lane's own bit (its lane id is threadIdx.x & 63)
 inline unsigned long long __ballot(int x) { return x ? 1ull << (threadIdx.x & 63) : 0ull; }
