@@ -533,7 +533,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
   // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE"})
+  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:
@@ -543,7 +543,11 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   int narrow = 3;
   if (const char* v = std::getenv("CEP_DEWEY_PAIRS"))
     if (std::atoi(v) > 0) narrow = std::atoi(v);
-  o += "#ifndef CEP_DEWEY_PAIRS\n#define CEP_DEWEY_PAIRS " + std::to_string(narrow) + "\n#endif\n";
+  o += "#ifndef CEP_DEWEY_PAIRS\n#define CEP_DEWEY_PAIRS " + std::to_string(narrow) + "\n";
+  // a single query's narrow build never runs persistent lanes (session.cpp: only kernel groups
+  // and the re-runs, which take the wide build, do): its kernel holds run() alone, half the code
+  if (!lits.param) o += "#ifndef CEP_PERSIST_LANES\n#define CEP_PERSIST_LANES 0\n#endif\n";
+  o += "#endif\n";
   o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
   if (lits.param) o += "#define CEP_WALK_COMPAT2 1  // kernel group: the wider straight-line walk step\n";
   o += "#include \"dewey.h\"\n#include \"java.h\"\n#include \"nfa_lane.h\"\n\nnamespace cep {\nnamespace {\n\n";
@@ -737,9 +741,9 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
         const std::string TI = std::to_string(E.target);
         f += "    if (" + m + ") {\n";
         if (T.sk != S.sk) {
-          f += "      if (!branching) {\n        Dewey v2 = ver;\n        if (!dw_add_stage(v2)) { L.err = kDwFull; return; }\n";
-          f += "        E" + TI + "(L, top, v2, false, " + SK + ", ev, w, o);\n      } else {\n";
-          f += "        E" + TI + "(L, top, ver, true, " + SK + ", ev, w, o);\n      }\n";
+          // one inlined copy of the target's code: addStage unless the run is branching
+          f += "      Dewey v2 = ver;\n      if (!branching && !dw_add_stage(v2)) { L.err = kDwFull; return; }\n";
+          f += "      E" + TI + "(L, top, v2, branching, " + SK + ", ev, w, o);\n";
         } else {
           f += "      E" + TI + "(L, top, ver, branching, " + SK + ", ev, w, o);\n";
         }
@@ -787,10 +791,11 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   for (uint32_t s = 0; s < d.n_stages; s++) {
     if (d.st[s].type == ST_FINAL) continue;
     const std::string SI = std::to_string(s), SK = std::to_string(d.st[s].sk);
-    o += "        case " + SI + ":\n          if (esk != " + SK + "u && !brf) {\n            Dewey v2 = c.ver;\n";
-    o += "            if (!dw_add_stage(v2)) { L.err = kDwFull; return -1; }\n";
-    o += "            E" + SI + "(L, top, v2, false, esk, ev, w, o);\n          } else {\n";
-    o += "            E" + SI + "(L, top, c.ver, brf, esk, ev, w, o);\n          }\n          break;\n";
+    // (one inlined copy of the stage's code per case: the version is addStage'd first when the
+    // record's epsilon stage differs from its target and the run is not branching)
+    o += "        case " + SI + ": {\n          Dewey v2 = c.ver;\n";
+    o += "          if (esk != " + SK + "u && !brf && !dw_add_stage(v2)) { L.err = kDwFull; return -1; }\n";
+    o += "          E" + SI + "(L, top, v2, brf, esk, ev, w, o);\n          break;\n        }\n";
   }
   o += "        default: L.err = KE_CAPACITY; return -1;\n      }\n    } else {\n";
   o += "      E" + std::to_string(d.begin_stage) + "(L, top, c.ver, brf, kNoSk, ev, w, o);\n    }\n";
@@ -841,7 +846,18 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
-    o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n}\n\n";
+    o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n";
+    // the watermark's second level: the first (at most) 1024 blocks each reduce a strided
+    // share of the bitmap blocks' maxima, one atomicMax per block (one per wave of a full
+    // pass cost 10 ms on one word: DESIGN.md)
+    o += "  if (A.wmax) {\n    const uint64_t R = gridDim.x < 1024 ? gridDim.x : 1024;\n";
+    o += "    if (blockIdx.x < R && threadIdx.x < 64) {  // (wave 0's key 4 * blockIdx.x < n_keys)\n      int64_t m = INT64_MIN;\n";
+    o += "      for (uint64_t i = blockIdx.x + R * (threadIdx.x & 63); i < A.n_wm_blocks; i += R * 64)\n";
+    o += "        m = A.wm_blocks[i] > m ? A.wm_blocks[i] : m;\n";
+    o += "      for (int o = 32; o > 0; o >>= 1) {\n        const int64_t y = __shfl_down(m, o, 64);\n";
+    o += "        m = y > m ? y : m;\n      }\n";
+    o += "      if (threadIdx.x == 0) atomicMax(A.wmax, (unsigned long long)m ^ 0x8000000000000000ull);\n";
+    o += "    }\n  }\n}\n\n";
     // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
     // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).
     // kBitStrips 256-position strips per block, their loads issued together (one position
@@ -854,7 +870,16 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "    const uint64_t p = p0 + (uint64_t)k * 256;\n    h[k] = p < A.n_events && begin_hit_at(A, p);\n  }\n";
     o += "#pragma unroll\n  for (int k = 0; k < S; k++) {\n    const uint64_t p = p0 + (uint64_t)k * 256;\n";
     o += "    const uint64_t b = __ballot(h[k]);\n";
-    o += "    if ((threadIdx.x & 63) == 0 && p < A.n_events) A.bhits[p >> 6] = b;\n  }\n}\n\n";
+    o += "    if ((threadIdx.x & 63) == 0 && p < A.n_events) A.bhits[p >> 6] = b;\n  }\n";
+    // the watermark's first level (session.cpp folds it here when the batch has timestamps):
+    // the block's largest event time, its S loads per thread issued together
+    o += "  if (A.wm_blocks) {\n    int64_t t[S];\n#pragma unroll\n    for (int k = 0; k < S; k++) {\n";
+    o += "      const uint64_t p = p0 + (uint64_t)k * 256;\n      t[k] = p < A.n_events ? A.ts[p] : INT64_MIN;\n    }\n";
+    o += "    int64_t m = t[0];\n#pragma unroll\n    for (int k = 1; k < S; k++) m = t[k] > m ? t[k] : m;\n";
+    o += "    for (int o = 32; o > 0; o >>= 1) {\n      const int64_t y = __shfl_down(m, o, 64);\n      m = y > m ? y : m;\n    }\n";
+    o += "    __shared__ int64_t wm[4];\n    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;\n    __syncthreads();\n";
+    o += "    if (threadIdx.x == 0) {\n      int64_t x = wm[0];\n      for (int i = 1; i < 4; i++) x = wm[i] > x ? wm[i] : x;\n";
+    o += "      A.wm_blocks[blockIdx.x] = x;\n    }\n  }\n}\n\n";
   }
   o += "}  // namespace cep\n";
   return o;

@@ -38,6 +38,8 @@ struct NfaArgs {
   const uint32_t* order;     // key of each rank (longest-first lane order), null = identity
   uint32_t* job_next;        // persistent lanes (nfa_lane.h run_jobs): next job index to claim;
                              // null: one job per lane (streaming sessions)
+  uint64_t spread;           // W > 0: an underfilled single-query launch of W waves, wave w's lane l
+                             // running rank l * W + w (session.cpp run_nfa); 0: rank w * 64 + l
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
@@ -55,6 +57,12 @@ struct NfaArgs {
   uint32_t* n_capacity_err;  // jobs to re-run (KE_RETRY / KE_CONFLICT)
   uint32_t* full;            // bit 0: a run queue overflowed this launch (the next batch starts
                              // with a bigger one, session.cpp)
+  // watermark folded into the bitmap pass (session.cpp): cep_nfa_bits writes each block's
+  // largest event time (of `ts`) to wm_blocks[block] (n_wm_blocks of them); cep_nfa_est's first
+  // blocks reduce them into *wmax (order-preserving unsigned map, one atomicMax per block)
+  int64_t* wm_blocks;
+  uint64_t n_wm_blocks;
+  unsigned long long* wmax;
   unsigned long long* prof;  // measurement builds ($CEP_PROF): the time split of nfa_lane.h, 16 counters
 };
 

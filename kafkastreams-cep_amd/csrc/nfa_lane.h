@@ -86,6 +86,7 @@ extern uint64_t cep_lane_stats[8];  // events, records, walks, walk nodes, pred 
 //   3 begin run             4 finals + queue swap          5 final drain
 //   6 waves                 7 whole run()                  8 loop iterations   9 records stepped
 //   10 lane-events (event() entered)                        11 walk nodes
+//   12 max over waves of the wave's lifetime (cycles)       13 the same in wall-clock ticks (100 MHz)
 #ifdef CEP_PROF
 #define CEP_PT(v) const uint64_t v = clock64()
 #define CEP_PACC(i, d) (prof[i] += (d))
@@ -159,9 +160,14 @@ struct RecLayout {
 
 // LDS slots per queue half for a record layout: 192 B of LDS per lane (48 KiB per 256-lane
 // block keeps 3 blocks = 3 waves per SIMD resident), at most 2 slots
+// ($CEP_RING_LDS_SLOTS at query compile: measurement runs)
 template <class Lay>
 __host__ __device__ constexpr int ring_lds_slots() {
+#ifdef CEP_RING_LDS_SLOTS
+  return CEP_RING_LDS_SLOTS;
+#else
   return (192 / (2 * 16 * Lay::kLdsQuads)) < 2 ? (192 / (2 * 16 * Lay::kLdsQuads)) : 2;
+#endif
 }
 
 // bytes of double-buffered run queues for n_slots lanes of rcap records (64-bit folds: the
@@ -213,13 +219,16 @@ struct Lane {
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
 #ifdef CEP_PROF
-  unsigned long long prof[12] = {};  // the time split (see CEP_PROF above), this wave / lane
+  unsigned long long prof[14] = {};  // the time split (see CEP_PROF above), this wave / lane
   // lane 0 adds the wave's cycles, the lane counters summed over the wave
   __device__ void prof_flush() {
     for (int i = 9; i < 12; i++)
       for (int o = 32; o > 0; o >>= 1) prof[i] += __shfl_xor(prof[i], o, 64);
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 0) {
       for (int i = 0; i < 12; i++) atomicAdd(A.prof + i, prof[i]);
+      atomicMax(A.prof + 12, prof[12]);
+      atomicMax(A.prof + 13, prof[13]);
+    }
   }
 #endif
 
@@ -1052,6 +1061,9 @@ struct Lane {
   // the whole key in one go (streaming sessions: one key per lane and launch)
   __device__ __forceinline__ void run() {
     CEP_PT(tr0);
+#ifdef CEP_PROF
+    const uint64_t tw0 = wall_clock64();
+#endif
     jj = j0;
     jn = j0 + n_ev;
     pa_err = KE_OK;
@@ -1078,6 +1090,8 @@ struct Lane {
     CEP_PACC(5, tr2 - tr1);
     CEP_PACC(6, 1);
     CEP_PACC(7, tr2 - tr0);
+    prof[12] = tr2 - tr0;
+    prof[13] = wall_clock64() - tw0;
     if (A.prof) prof_flush();
 #endif
   }
@@ -1172,6 +1186,9 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   constexpr uint32_t kClaim = 128;
   uint64_t wnext = 0, wend = 0;
   CEP_PT(tr0);
+#ifdef CEP_PROF
+  const uint64_t tw0 = wall_clock64();
+#endif
   for (;;) {
     CEP_LPACC(L, 8, 1);
     const uint64_t need = __ballot(!has && !drained);
@@ -1241,18 +1258,25 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   CEP_PT(tr1);
   CEP_LPACC(L, 6, 1);
   CEP_LPACC(L, 7, tr1 - tr0);
+  L.prof[12] = tr1 - tr0;
+  L.prof[13] = wall_clock64() - tw0;
   if (A.prof) L.prof_flush();
 #endif
 }
 
 // Driver shared by the AOT and JIT kernels: slot -> key, initial or carried state, the
 // batch's events of the key, KeyState (and KeyCarry for the next batch of a stream).
+#ifndef CEP_PERSIST_LANES
+#define CEP_PERSIST_LANES 1
+#endif
 template <int F, class Q>
 __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullptr) {
+#if CEP_PERSIST_LANES
   if (A.job_next) {  // per-batch sessions: persistent lanes over the job list
     run_jobs<F>(A, q, lds);
     return;
   }
+#endif
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t job;
   if (A.jobs) {
@@ -1261,7 +1285,8 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   } else {
     const uint32_t nq = A.n_q ? A.n_q : 1;
     const uint64_t w = slot / 64;
-    const uint64_t rank = (w / nq) * 64 + slot % 64;
+    // spread: the heaviest W keys (lane order) lead one wave each, the next W are their lanes 1, ...
+    const uint64_t rank = A.spread ? (slot % 64) * A.spread + w : (w / nq) * 64 + slot % 64;
     if (rank >= A.n_keys) return;
     job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
   }

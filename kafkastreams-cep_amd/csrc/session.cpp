@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -42,11 +43,28 @@ struct HipError : std::runtime_error {
   } while (0)
 
 // A grow-only device buffer.
+// $CEP_HOST_TRACE (measurement runs): device (re)allocations and push phases on stderr, ms
+static bool host_trace() {
+  static const bool on = std::getenv("CEP_HOST_TRACE") != nullptr;
+  return on;
+}
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct DBuf {
   void* p = nullptr;
   size_t bytes = 0;
   void ensure(size_t n) {
     if (n <= bytes) return;
+    const double t0 = host_trace() ? now_ms() : 0;
+    struct Tr {
+      double t0;
+      size_t n;
+      ~Tr() {
+        if (host_trace()) std::fprintf(stderr, "cep_host alloc %zu B %.2f ms\n", n, now_ms() - t0);
+      }
+    } tr{t0, n};
     if (p) HIPCHECK(hipFree(p));
     p = nullptr;
     bytes = 0;
@@ -60,6 +78,14 @@ struct DBuf {
   // grow keeping the first `keep` bytes
   void grow_keep(size_t n, size_t keep, hipStream_t st) {
     if (n <= bytes) return;
+    const double t0 = host_trace() ? now_ms() : 0;
+    struct Tr {
+      double t0;
+      size_t n;
+      ~Tr() {
+        if (host_trace()) std::fprintf(stderr, "cep_host grow %zu B %.2f ms\n", n, now_ms() - t0);
+      }
+    } tr{t0, n};
     void* q = nullptr;
     if (hipMalloc(&q, n) != hipSuccess) throw std::bad_alloc();
     if (p && keep) HIPCHECK(hipMemcpyAsync(q, p, std::min(keep, bytes), hipMemcpyDeviceToDevice, st));
@@ -195,6 +221,8 @@ struct cep_session {
   int64_t watermark = INT64_MIN;
   unsigned long long* h_wm = nullptr;  // pinned: the batch's max timestamp (read by resolve())
   bool wm_pending = false;
+  bool wm_fold = false;  // this batch's watermark comes from the first group's bitmap/estimate passes
+  DBuf wm_blocks;        // their per-block maxima
   // arrival-order batches: device copies of the input, the partitioned (CSR) batch
   DBuf a_keys, a_ts, p_off, p_cnt, p_ts, p_perm, p_sorted, p_idx, p_scratch;
   DBuf a_cols[kMaxFields], p_cols[kMaxFields];
@@ -385,11 +413,22 @@ void run_nfa(cep_session* s, GroupRt& g) {
     if (std::atoi(e) > 0) waves_cu = (uint64_t)std::atoi(e);
   const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
   auto grid_for = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident); };
-  // $CEP_NO_PERSIST / $CEP_PERSIST (measurement runs): one lane per job / persistent lanes
-  // (single queries run one lane per key: their longest-first lane order already balances the
-  // waves, and persistent lanes cost cfg 3 ~35 %; groups mix light and heavy queries)
-  const bool persist = !streaming && !std::getenv("CEP_NO_PERSIST") && (Q > 1 || std::getenv("CEP_PERSIST"));
-  const uint64_t slots = !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
+  // $CEP_NO_PERSIST (measurement runs): one lane per job.  Single queries run one lane per key:
+  // their longest-first lane order already balances the waves (persistent lanes cost cfg 3
+  // ~35 %), and their narrow kernel is built without the persistent driver; groups mix light
+  // and heavy queries.
+  const bool persist = !streaming && !std::getenv("CEP_NO_PERSIST") && Q > 1;
+  // An underfilled single-query launch (fewer waves than the chip holds: a shard of a
+  // multi-GPU run, a small batch) is as long as its longest wave, whose length is its heaviest
+  // key's chain of events times the wave's per-event cost; that cost grows with the number of
+  // divergent lanes.  So its keys are spread over every wave slot the chip holds: the heaviest
+  // keys lead one wave each, with lighter keys beside them ($CEP_SPREAD=0: measurement runs).
+  uint64_t spread = 0;
+  if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64) {
+    const char* e = std::getenv("CEP_SPREAD");
+    if (!e || std::atoi(e) != 0) spread = std::min<uint64_t>(resident / 64, nk);
+  }
+  const uint64_t slots = spread ? spread * 64 : !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
@@ -407,13 +446,15 @@ void run_nfa(cep_session* s, GroupRt& g) {
     if (std::atoi(e) > 0) ochunk = (uint32_t)std::atoi(e);
   const uint32_t pchunk = nchunk;
   const uint64_t ev_q = (uint64_t)((double)s->n_events * (double)Q);
-  uint64_t node_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_nodes * 3 / 2 + 4096);
-  uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096, g.last_preds * 3 / 2 + 4096);
-  uint64_t out_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q * 2 / kOutChunkWords) + jobs / 64 + 1024,
+  // (the last batch's pool tops already count the ranges lanes held at its end; the estimate
+  // from pool_factor adds them: a steady stream of like batches never reallocates)
+  uint64_t node_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096 + slots * nchunk,
+                                         g.last_nodes * 3 / 2 + 4096);
+  uint64_t pred_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q) + 4096 + slots * pchunk,
+                                         g.last_preds * 3 / 2 + 4096);
+  uint64_t out_cap = std::max<uint64_t>((uint64_t)(pf * (double)ev_q * 2 / kOutChunkWords) + jobs / 64 + 1024 +
+                                            slots * ochunk,
                                         g.last_out * 3 / 2 + 1024);
-  node_cap += slots * nchunk;  // ranges in hand at the end of the launch
-  pred_cap += slots * pchunk;
-  out_cap += slots * ochunk;
   node_cap = std::min<uint64_t>(node_cap, kNodeMax);
   pred_cap = std::min<uint64_t>(pred_cap, kNodeMax);
   out_cap = std::min<uint64_t>(out_cap, kPoolMax);  // chunk ids are u32, word addresses u64
@@ -438,9 +479,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
       HIPCHECK(hipMemsetAsync(S.carry.p, 0, sizeof(KeyCarry) * std::max<uint64_t>(nk, 1), s->stream));
       S.tops.ensure(2 * sizeof(uint32_t));
       HIPCHECK(hipMemsetAsync(S.tops.p, 0, 2 * sizeof(uint32_t), s->stream));
-      S.rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
+      // a stream's run queues live at their key's position (nfa_lane.h run_key), whatever the
+      // launch's slot count (an underfilled launch spreads its keys over more slots)
+      S.rings.ensure(ring_size(g.F, std::max<uint64_t>(nk, 1), rcap));
       S.rcap = rcap;
-      S.ring_bytes = ring_size(g.F, std::max<uint64_t>(slots, 1), rcap);
+      S.ring_bytes = ring_size(g.F, std::max<uint64_t>(nk, 1), rcap);
       S.init = true;
     } else if (nk != S.n_keys) {
       throw std::invalid_argument("the batches of a streaming session share one key space (n_keys)");
@@ -479,6 +522,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.wcap = wcap;
   a.defer = 1;
   a.n_q = (uint32_t)Q;
+  a.spread = spread;
   a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
   a.preds = s->preds.as<Pred>();
@@ -510,10 +554,18 @@ void run_nfa(cep_session* s, GroupRt& g) {
   float total_ms = 0;
   uint32_t launches = 0;
   HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  const bool wm_here = s->wm_fold && &g == s->groups[0].get();
   if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
     s->bhits.ensure(8 * ((s->n_events + 63) / 64));
     a.bhits = s->bhits.as<uint64_t>();
-    HIPCHECK(launch_fn(g.fn_bits, a, (s->n_events + 256 * kBitStrips - 1) / (256 * kBitStrips), s->stream));
+    const uint64_t nb = (s->n_events + 256 * kBitStrips - 1) / (256 * kBitStrips);
+    if (wm_here) {  // (run_nfa's scratch memset above cleared wmax)
+      s->wm_blocks.ensure(8 * nb);
+      a.wm_blocks = s->wm_blocks.as<int64_t>();
+      a.n_wm_blocks = nb;
+      a.wmax = &sc->wmax;
+    }
+    HIPCHECK(launch_fn(g.fn_bits, a, nb, s->stream));
   }
   // Lane order: keys sorted by estimated work, longest first (cep_nfa_est, from the begin-hit bitmap), so a wave's 64
   // lanes carry similar work (a wave lasts as long as its longest lane) and the longest waves
@@ -526,6 +578,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     g.order_tmp.ensure(4 * nk);
     a.est = g.est.as<uint32_t>();
     HIPCHECK(launch_fn(g.fn_est, a, (nk + 3) / 4, s->stream));  // a wave per key
+    a.wmax = nullptr;  // (reduced once; wm_blocks stays set: no other kernel reads it)
     HIPCHECK(sort_keys_by_work(g.est.as<uint32_t>(), g.est_sorted.as<uint32_t>(), g.order_tmp.as<uint32_t>(),
                                g.order.as<uint32_t>(), nk, g.sort_tmp, g.sort_tmp_bytes, s->stream));
     a.order = g.order.as<uint32_t>();
@@ -546,11 +599,12 @@ void run_nfa(cep_session* s, GroupRt& g) {
   Scratch h{};
   HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
+  if (wm_here) s->watermark = (int64_t)(h.wmax ^ 0x8000000000000000ull);
   if (prof) {  // one line per launch on stderr: the counters of nfa_lane.h's CEP_PROF list
     unsigned long long pc[16];
     HIPCHECK(hipMemcpy(pc, s->prof.p, sizeof pc, hipMemcpyDeviceToHost));
     std::fprintf(stderr, "cep_prof {\"jobs\": %llu, \"c\": [", (unsigned long long)jobs);
-    for (int i = 0; i < 12; i++) std::fprintf(stderr, "%s%llu", i ? ", " : "", pc[i]);
+    for (int i = 0; i < 14; i++) std::fprintf(stderr, "%s%llu", i ? ", " : "", pc[i]);
     std::fprintf(stderr, "]}\n");
     a.prof = nullptr;
   }
@@ -631,6 +685,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.rings = s->retry_rings.p;
     a.walks = s->walks.p;
     a.order = nullptr;
+    a.spread = 0;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
     for (int k = 0; k < 2; k++) {  // capacity re-runs keep deferred walks, conflicts walk in place
       if (!lens[k]) continue;
@@ -1016,7 +1071,9 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     s->partition_ms = 0;
     s->layout_host_valid = false;
     if (s->arrival) {
+      const double t0 = host_trace() ? now_ms() : 0;
       partition_batch(s, b);
+      if (host_trace()) std::fprintf(stderr, "cep_host partition %.2f ms\n", now_ms() - t0);
     } else if (b->memory == CEP_MEM_DEVICE) {
       s->key_off = b->key_off;
       for (uint32_t f = 0; f < nf; f++) s->cols.p[f] = b->cols[f];
@@ -1044,10 +1101,14 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       // memory) must be done before returning, even when only stencil work follows
       HIPCHECK(hipStreamSynchronize(s->stream));
     }
-    // watermark
+    // watermark.  When the batch runs an NFA group with a begin-hit bitmap and a lane order,
+    // the max is folded into those passes (run_nfa: block maxima in cep_nfa_bits, reduced by
+    // cep_nfa_est), which stream the batch anyway; otherwise its own pass over the timestamps
     s->watermark = INT64_MIN;
     s->wm_pending = false;
-    if (s->ts && s->n_events) {  // read back with the batch's other results (resolve())
+    s->wm_fold = s->ts && s->n_events && !s->groups.empty() && s->groups[0]->fn_bits && s->groups[0]->fn_est &&
+                 s->n_keys > 64 && !std::getenv("CEP_NO_WM_FOLD");
+    if (s->ts && s->n_events && !s->wm_fold) {  // read back with the batch's other results (resolve())
       s->scratch.ensure(sizeof(Scratch));
       Scratch* sc = s->scratch.as<Scratch>();
       if (!s->h_wm) HIPCHECK(hipHostMalloc((void**)&s->h_wm, sizeof(unsigned long long), hipHostMallocDefault));
@@ -1063,7 +1124,9 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
       throw std::invalid_argument("queries x keys of a batch must stay below 2^32 (job ids are u32)");
     for (auto& r : s->qs)  // a stream carries NFA state between batches: stencil queries run on the NFA there
       if (r->group < 0) run_stencil(s, *r);
+    const double t0 = host_trace() ? now_ms() : 0;
     for (auto& g : s->groups) run_nfa(s, *g);
+    if (host_trace()) std::fprintf(stderr, "cep_host run_nfa %.2f ms\n", now_ms() - t0);
     for (auto& r : s->qs) r->have = true;
   });
 }

@@ -48,7 +48,7 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False):
             f.write(src)
         tmp = so + f".{os.getpid()}"
         subprocess.check_call([CLANG, "-x", "c++", "-std=c++17", "-O1", "-g", "-rdynamic", "-shared", "-fPIC",
-                               "-ffp-contract=off", "-Wno-unused-value", "-w", "-DCEP_LANE_STATS",
+                               "-ffp-contract=off", "-Wno-unused-value", "-w", "-DCEP_LANE_STATS", "-DCEP_PERSIST_LANES=1",
                                f"-I{os.path.join(HERE, 'lane_cpu')}", f"-I{CSRC}",
                                f'-DQUERY_SRC="{qsrc}"', os.path.join(HERE, "lane_cpu", "driver.cpp"),
                                "-o", tmp])

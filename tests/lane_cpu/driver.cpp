@@ -13,7 +13,7 @@
 
 #include QUERY_SRC
 
-thread_local LaneDim3 blockIdx, threadIdx, blockDim;
+thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
 uint64_t cep_lane_stats[8];
 extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
 

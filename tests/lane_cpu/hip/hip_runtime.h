@@ -18,11 +18,16 @@
 struct LaneDim3 {
   unsigned x = 0, y = 0, z = 0;
 };
-extern thread_local LaneDim3 blockIdx, threadIdx, blockDim;
+extern thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
 
 inline unsigned atomicAdd(unsigned* p, unsigned v) {
   const unsigned o = *p;
   *p += v;
+  return o;
+}
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+  const unsigned long long o = *p;
+  if (v > o) *p = v;
   return o;
 }
 inline unsigned atomicOr(unsigned* p, unsigned v) {
@@ -30,6 +35,7 @@ inline unsigned atomicOr(unsigned* p, unsigned v) {
   *p = o | v;
   return o;
 }
+inline void __syncthreads() {}  // one lane at a time
 inline bool __any(int x) { return x != 0; }  // a wave of one lane
 // a wave of one lane: the calling lane's own bit (its lane id is threadIdx.x & 63)
 inline unsigned long long __ballot(int x) { return x ? 1ull << (threadIdx.x & 63) : 0ull; }

@@ -370,6 +370,29 @@ def test_watermark():
     assert s2.watermark() == -7 + d.n_events
 
 
+def test_watermark_folded():
+    """> 64 keys: the watermark comes from the bitmap pass's block maxima reduced by the
+    estimate pass (session.cpp wm_fold), not from its own pass; the maximum in the first,
+    a middle and the last event, batch sizes around the bitmap block (4096 events), unaligned
+    device timestamps."""
+    q = N.Query(W.stock_query("readme").to_ir())
+    s = N.Session(q)
+    rng = np.random.default_rng(12)
+    for nk, mean in ((65, 3), (100, 41), (1000, 40), (3000, 700)):
+        d = N.synth_stream("stock", 7, nk, mean)
+        off, cols = d.download()
+        n = d.n_events
+        for where in (0, n // 2, n - 1):
+            ts = rng.integers(-(1 << 40), 1 << 40, n)
+            ts[where] = (1 << 41) + n
+            s.push(off, cols, ts=ts)
+            assert s.watermark() == (1 << 41) + n, (nk, n, where)
+    d = N.synth_stream("stock", 5, 400, 30)
+    t = N.synth_ts(d.n_events + 1, -7)
+    s.push_device(d, t.ptr + 8)
+    assert s.watermark() == -7 + d.n_events
+
+
 def test_cfg2_full_size_checksum():
     """Config 2 at its BASELINE size (1e8 events over 1e4 keys, generated in HBM): the
     stencil's match count and checksum equal the oracle's on the same stream."""
