@@ -1,38 +1,52 @@
-"""HBM bytes per launch for bench.py's `roofline.traffic`, from a profiles/summarize.py
-summary (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, KiB per dispatch).
+"""HBM bytes per launch for bench.py's `roofline.traffic`, from rocprofv3 FETCH_SIZE and
+WRITE_SIZE passes (separate runs, KiB per dispatch in run_counter_collection.csv).
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
-coalesced streaming reads -> x2 for the stencil passes (calibrated there: stencil_mask's
-corrected fetch equals its 400 MB column + 12.5 MB bitmap).  The NFA kernel's reads are
-per-lane scattered; the guide leaves such widths uncalibrated, so its FETCH_SIZE is taken
-as is (a lower bound).  WRITE_SIZE is exact for 16-B stores and taken as is.
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read, so every kernel's fetch is doubled - applied to all kernels alike
+(the NFA's reads are mostly per-lane 16-B quads; for narrower or scattered reads the doubled
+figure is an upper bound).  WRITE_SIZE is taken as is (exact for 16-B stores).
 
-The JSON decoder stages its byte span with 16-B coalesced loads: FETCH_SIZE x 2 as for the
-stencil.
+Per kernel the median over its dispatches is taken (the first push of a session may run a
+smaller or a re-run launch); a key may sum several kernels (a whole step).
 
-usage: python profiles/traffic.py summary.json [more summaries...] > profiles/pmc_traffic.json
-(a kernel is taken from the first summary that has it)
+usage: python profiles/traffic.py OUT.json KEY:FETCH_DIR:WRITE_DIR:KERNEL[+KERNEL...][/PUSHES] ...
+  e.g. cep_nfa_jit_cfg4s:profiles/r03/pmc_cfg4s_FETCH_SIZE:profiles/r03/pmc_cfg4s_WRITE_SIZE:cep_nfa_jit
+An existing OUT.json keeps its other keys.
 """
+import csv
 import json
+import os
+import statistics
 import sys
+from collections import defaultdict
 
-STENCIL = ("stencil_mask", "stencil_scan", "stencil_emit")
+
+def per_kernel(d, pushes=0):
+    """median bytes per dispatch of each kernel; pushes > 0: the sum over its dispatches / pushes
+    (a push whose main launch is followed by re-run launches)"""
+    acc = defaultdict(list)
+    with open(os.path.join(d, "run_counter_collection.csv")) as f:
+        for r in csv.DictReader(f):
+            acc[r["Kernel_Name"].split("(")[0].replace("cep::", "")].append(float(r["Counter_Value"]) * 1024)
+    return {k: (sum(v) / pushes if pushes else statistics.median(v)) for k, v in acc.items()}
 
 
-def main(paths):
-    out = {"_source": " ".join(paths), "_unit": "bytes per launch (HBM, rocprofv3 PMC)"}
-    for path in paths:
-        s = json.load(open(path))
-        for name, row in s.items():
-            if name.startswith("cep_nfa_jit") and "FETCH_SIZE" in row and "cep_nfa_jit" not in out:
-                out["cep_nfa_jit"] = row["FETCH_SIZE"] * 1024 + row["WRITE_SIZE"] * 1024
-            if name == "decode_stock_json_kernel" and "FETCH_SIZE" in row and name not in out:
-                out[name] = 2 * row["FETCH_SIZE"] * 1024 + row["WRITE_SIZE"] * 1024
-        st = [row for name, row in s.items() if name.startswith(STENCIL) and "FETCH_SIZE" in row]
-        if st and "stencil" not in out:
-            out["stencil"] = sum(2 * r["FETCH_SIZE"] * 1024 + r["WRITE_SIZE"] * 1024 for r in st)
-    print(json.dumps(out, indent=1))
+def main(out, specs):
+    res = json.load(open(out)) if os.path.exists(out) else {}
+    res["_unit"] = "bytes per launch (HBM, rocprofv3 PMC): traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction)"
+    for spec in specs:
+        key, fd, wd, kernels = spec.split(":")
+        kernels, _, pushes = kernels.partition("/")
+        fetch, write = per_kernel(fd, int(pushes or 0)), per_kernel(wd, int(pushes or 0))
+        ks = kernels.split("+")
+        f = sum(fetch[k] for k in ks)
+        w = sum(write[k] for k in ks)
+        res[key] = 2 * f + w
+        res["_" + key] = {"kernels": ks, "fetch_raw": f, "write": w, "source": [fd, wd]}
+    with open(out, "w") as fo:
+        json.dump(res, fo, indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    main(sys.argv[1], sys.argv[2:])
