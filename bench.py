@@ -151,10 +151,13 @@ def load_traffic(name):
         return None
 
 
-def roofline(alg_bytes, kernel_ms, kernel, traffic_key=None, **extra):
+def roofline(alg_bytes, kernel_ms, kernel, traffic_key=None, traffic_scale=1, **extra):
+    """traffic: the committed PMC figure for one launch (x traffic_scale launches per priced
+    interval, e.g. config 5's key-range batches per step)"""
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    tr = load_traffic(traffic_key or kernel)
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-         "traffic": load_traffic(traffic_key or kernel), "kernel": kernel, "kernel_ms": kernel_ms,
+         "traffic": tr * traffic_scale if tr is not None else None, "kernel": kernel, "kernel_ms": kernel_ms,
          "algorithmic_bytes": alg_bytes}
     r.update(extra)
     return r
@@ -453,7 +456,8 @@ def cfg5(device, n_keys, sub, steps, warmup, threads, cpu_every):
            "ms_per_step": 1e3 * tot["wall"] / steps, "matches_per_step": tot["matches"] // steps,
            "pairs_per_step": tot["pairs"] // steps, "key_errors": tot["errors"] // steps,
            "retried_jobs": tot["retried"], "kernel_ms_per_step": tot["kernel_ms"] / steps,
-           "roofline": roofline(alg, tot["kernel_ms"], "cep_nfa_jit (64-query group)", "cep_nfa_jit_cfg5")}
+           "roofline": roofline(alg, tot["kernel_ms"], "cep_nfa_jit (64-query group)", "cep_nfa_jit_cfg5",
+                                traffic_scale=len(parts))}
     if cpu_every:
         log("cfg5 cpu baseline")
         c = W.SynthConfig("cfg5", "stock", n_keys, 1000, cfg.seed)

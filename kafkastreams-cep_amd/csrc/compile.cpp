@@ -712,45 +712,75 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     f += "    const bool br = (" + hasP + " && " + hasT + ") || (" + hasI + " && " + hasT + ") || (" + hasI + " && " + hasB +
          ") || (" + hasI + " && " + hasP + ");\n";
     f += "    bool consumed = false, ignored = false;\n    (void)consumed; (void)ignored;\n";
+    // Not branching, at most one edge matched (isBranching holds for every pair of edges a stage
+    // can have: {T,P} {I,T} {I,B} {I,P}): the consuming edge (TAKE: eps(cur -> cur); BEGIN:
+    // eps(cur -> target)) and IGNORE (the record again) share one push_rec - the wave runs one
+    // copy of it whichever edge each lane took.
+    std::string cons = "false", consWord, procTarget;
+    int procTI = -1;
     for (int e = 0; e < S.n_edges; e++) {
       const DevEdge& E = S.e[e];
       const std::string m = "m" + std::to_string(e);
       if (E.op == OP_TAKE) {
-        f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        const uint32_t nd = L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n";
-        f += "        if (L.err) return;\n";
-        f += "        const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + SI + "u, L.j, CEP_NONE, ver, nd);\n";
-        f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n";
-        f += "      } else {\n";
-        f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = kDwFull; return; }\n";
-        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2, top.hsk, top.node);\n      }\n";
-        f += "      if (L.err) return;\n      consumed = true;\n    }\n";
+        cons = m;
+        consWord = "kRecEps | (" + SK + "u << 8) | " + SI + "u";
       } else if (E.op == OP_BEGIN) {
-        const bool fin = d.st[E.target].type == ST_FINAL;
-        f += "    if (" + m + ") {\n      const uint32_t nd = L.put_link(" + SK +
-             ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n      if (L.err) return;\n";
-        f += "      const int r = L.push_rec(kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
-             (fin ? " | kRecFinal" : "") + ", L.j, CEP_NONE, ver, nd);\n";
-        f += "      if (r < 0) return;\n      o.same = r;\n      o.produced++;\n      consumed = true;\n    }\n";
-      } else if (E.op == OP_IGNORE) {
-        f += "    if (" + m + ") {\n      if (!br) {\n";
-        f += "        const int r = L.push_rec((top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u), top.event, top.ev_first, ver, top.node);\n";
-        f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n      }\n      ignored = true;\n    }\n";
-      } else {  // PROCEED
-        const DevStage& T = d.st[E.target];
-        const std::string TI = std::to_string(E.target);
-        f += "    if (" + m + ") {\n";
-        if (T.sk != S.sk) {
-          // one inlined copy of the target's code: addStage unless the run is branching
-          f += "      Dewey v2 = ver;\n      if (!branching && !dw_add_stage(v2)) { L.err = kDwFull; return; }\n";
-          f += "      E" + TI + "(L, top, v2, branching, " + SK + ", ev, w, o);\n";
-        } else {
-          f += "      E" + TI + "(L, top, ver, branching, " + SK + ", ev, w, o);\n";
-        }
-        f += "      if (L.err) return;\n    }\n";
+        cons = m;
+        consWord = "kRecEps | (" + SK + "u << 8) | " + std::to_string(E.target) + "u" +
+                   (d.st[E.target].type == ST_FINAL ? " | kRecFinal" : "");
+      } else if (E.op == OP_PROCEED) {
+        procTI = (int)E.target;
       }
     }
-    f += "    if (br) {\n      if (prev_sk == kNoSk) { L.err = KE_NPE; return; }\n";
+    auto proceed = [&](const std::string& indent) {
+      const DevStage& T = d.st[procTI];
+      const std::string TI = std::to_string(procTI);
+      std::string g;
+      if (T.sk != S.sk) {  // one inlined copy of the target's code: addStage unless the run is branching
+        g += indent + "Dewey v2 = ver;\n" + indent + "if (!branching && !dw_add_stage(v2)) { L.err = kDwFull; return; }\n";
+        g += indent + "E" + TI + "(L, top, v2, branching, " + SK + ", ev, w, o);\n";
+      } else {
+        g += indent + "E" + TI + "(L, top, ver, branching, " + SK + ", ev, w, o);\n";
+      }
+      g += indent + "if (L.err) return;\n";
+      return g;
+    };
+    f += "    if (!br) {\n";
+    f += "      if (" + cons + " || " + hasI + ") {\n";
+    f += "        uint32_t nd = top.node, sw = (top.stage & ~(kRecBranch | kRecFinal)) | (branching ? kRecBranch : 0u);\n";
+    f += "        uint32_t e0 = top.event, ef = top.ev_first;\n";
+    if (cons != "false") {
+      f += "        if (" + cons + ") {\n";
+      f += "          nd = L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n";
+      f += "          if (L.err) return;\n";
+      f += "          sw = " + consWord + ";\n          e0 = L.j;\n          ef = CEP_NONE;\n          consumed = true;\n        }\n";
+    }
+    f += "        const int r = L.push_rec(sw, e0, ef, ver, nd);\n";
+    f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n      }\n";
+    f += "    } else {\n";
+    // branching: every matched edge in edge order, then the branch record
+    for (int e = 0; e < S.n_edges; e++) {
+      const DevEdge& E = S.e[e];
+      const std::string m = "m" + std::to_string(e);
+      if (E.op == OP_TAKE) {
+        f += "      if (" + m + ") {\n";
+        f += "        Dewey v2 = ver;\n        if (!dw_add_run(v2)) { L.err = kDwFull; return; }\n";
+        f += "        L.put_link(" + SK + ", prev_sk, top.event, top.ev_first, v2, top.hsk, top.node);\n";
+        f += "        if (L.err) return;\n        consumed = true;\n      }\n";
+      } else if (E.op == OP_BEGIN) {
+        f += "      if (" + m + ") {\n        const uint32_t nd = L.put_link(" + SK +
+             ", prev_sk, top.event, top.ev_first, ver, top.hsk, top.node);\n        if (L.err) return;\n";
+        f += "        const int r = L.push_rec(" + consWord + ", L.j, CEP_NONE, ver, nd);\n";
+        f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n        consumed = true;\n      }\n";
+      } else if (E.op == OP_IGNORE) {
+        f += "      if (" + m + ") ignored = true;\n";
+      }
+    }
+    f += "    }\n";
+    // PROCEED (alone, or after the branching edges above): one inlined copy of the target
+    if (procTI >= 0) f += "    if (" + hasP + ") {\n" + proceed("      ") + "    }\n";
+    f += "    if (br) {\n";
+    f += "      // the branch record (NFA.java:231-246)\n      if (prev_sk == kNoSk) { L.err = KE_NPE; return; }\n";
     f += "      Dewey v2 = ver;\n      if (!dw_add_run(v2)) { L.err = kDwFull; return; }\n";
     f += "      const int r = L.push_rec(kRecEps | kRecBranch | (prev_sk << 8) | " + SI +
          "u, ignored ? top.event : L.j, ignored ? top.ev_first : CEP_NONE, v2, ignored && prev_sk == top.hsk ? top.node : CEP_NONE);\n      if (r < 0) return;\n";

@@ -64,17 +64,24 @@
 // observes a walk's effects: walks change refcounts, predecessor lists and live bits of
 // nodes of events before the walk's own event; the step only appends to nodes of the
 // current event and reads older nodes through put()'s predecessor lookup, which checks the
-// live bit.  That one read is checked: every such lookup stamps the node with the number of
-// walks queued so far, and a walk that deletes a node stamped after it was queued (the
-// reference would have thrown "Cannot find predecessor event") reports KE_CONFLICT; the key
-// is then re-run with walks in place (session.cpp).  Errors keep their reference order: a
-// walk's exception precedes anything the step did after queueing it.
+// live bit.  That one read is checked: a lookup made while walks are queued stamps the node
+// with the number of walks queued so far and appends (node, that number, event) to the lane's
+// put log.  A walk that deletes a node stamped after the walk was queued is exactly the
+// reference's "Cannot find predecessor event" (KVSharedVersionedBuffer.java:86-89): the node
+// is gone when the first put made after the walk looks it up, and nothing between the two
+// reads that node (nodes are only created at the current event; steps read older nodes only
+// through put()).  So the walk completes, the put log names that first put (its event and
+// walk count), the walks queued before it still run in order (their matches and exceptions
+// come first), and the key stops with IllegalState at the put's event - the result of
+// running the walks in place, without a re-run.  (A put log that would overflow mid-event
+// falls back to KE_CONFLICT: the key is re-run with walks in place, session.cpp.)  Errors keep
+// their reference order: a walk's exception precedes anything the step did after queueing it.
 #pragma once
 #include "dewey.h"
 
 // Work counters for the CPU lane build (tests/lane_cpu, CEP_LANE_STATS); nothing on the GPU.
 #ifdef CEP_LANE_STATS
-extern uint64_t cep_lane_stats[8];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters
+extern uint64_t cep_lane_stats[9];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters, exact conflicts
 #define CEP_STAT(i) (cep_lane_stats[i]++)
 #else
 #define CEP_STAT(i) ((void)0)
@@ -121,6 +128,9 @@ constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the 
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
+// put-log entries per lane ({node, walks queued, event, -}), after the walk queues in A.walks;
+// the wave drains its walks before an event could overflow it
+constexpr uint32_t kPutLog = 256;
 // a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
 // re-runs the job in the wide one (a retry); the wide build's limit is final
 constexpr int32_t kDwFull = kDeweyPairs < 6 ? KE_RETRY : KE_CAPACITY;
@@ -177,8 +187,12 @@ __host__ __device__ inline uint64_t ring_bytes(int F, uint64_t n_slots, uint32_t
   return ((n_slots + 63) / 64) * 64ull * 2ull * rcap * quads * 16ull;
 }
 
-// bytes of deferred-walk queues for n_slots lanes of wcap walks
+// bytes of deferred-walk queues for n_slots lanes of wcap walks, then their put logs
 __host__ __device__ inline uint64_t walkq_bytes(uint64_t n_slots, uint32_t wcap) {
+  return ((n_slots + 63) / 64) * 64ull * (wcap * kWalkQuads + kPutLog) * 16ull;
+}
+// the put logs' offset in that allocation
+__host__ __device__ inline uint64_t putlog_offset(uint64_t n_slots, uint32_t wcap) {
   return ((n_slots + 63) / 64) * 64ull * wcap * kWalkQuads * 16ull;
 }
 
@@ -200,6 +214,7 @@ struct Lane {
   v4u* rb;  // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
   lds_v4u* lr;  // LDS slots: this lane's quad 0 of half 0, slot 0 (stride 64 quads)
   v4u* wb;  // this lane's walk queue, slot 0 quad 0 (stride 64 quads)
+  v4u* pb;  // this lane's put log, entry 0 (stride 64 quads)
   uint32_t half = 0, count = 0, ocount = 0;  // input half, its records, records written
   uint32_t bdig = 1;                         // kBeginReg: the begin run's version "bdig"
   uint32_t n_final = 0;                      // finals queued at this event
@@ -217,6 +232,8 @@ struct Lane {
   // deferred walks
   uint32_t wq_n = 0;  // queued
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
+  uint32_t pl_n = 0;  // put-log entries since the last flush
+  uint32_t cut_opc = CEP_NONE, cut_ev = 0;  // the first put that a queued walk's delete makes throw
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
 #ifdef CEP_PROF
   unsigned long long prof[14] = {};  // the time split (see CEP_PROF above), this wave / lane
@@ -239,6 +256,11 @@ struct Lane {
   }
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
+  }
+  __device__ __forceinline__ v4u* PL(uint32_t i) const { return pb + (uint64_t)i * 64; }
+  // put-log entries one event may add at most (its records' puts): the wave drains before
+  __device__ __forceinline__ uint32_t plog_margin() const {
+    return 2 * A.rcap + 4 < kPutLog / 2 ? 2 * A.rcap + 4 : kPutLog / 2;
   }
   __device__ __forceinline__ lds_v4u* LQ(uint32_t h, uint32_t slot, int lq) const {
     return lr + ((h * kRL + slot) * Lay::kLdsQuads + lq) * 64;
@@ -504,7 +526,14 @@ struct Lane {
       err = KE_ILLEGAL_STATE;
       return CEP_NONE;
     }
-    if (A.defer) A.nodes[p].lk = opc;  // found live after `opc` queued walks (conflict check)
+    if (A.defer && wq_n > 0) {  // found live while walks are queued: stamp and log (conflict check)
+      if (pl_n >= kPutLog) {        // (only an event with more puts than plog_margin())
+        err = A.carry ? KE_CAPACITY : KE_CONFLICT;
+        return CEP_NONE;
+      }
+      A.nodes[p].lk = opc;
+      *PL(pl_n++) = v4u{p, opc, j, 0u};
+    }
     const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
     if (c == CEP_NONE) return new_node(sk, p, v);
     append_pred(c, p, v);
@@ -642,7 +671,7 @@ struct Lane {
       return;
     }
     if (wq_n >= A.wcap) {  // more walks in one event than the queue holds: re-run in place
-      err = KE_CONFLICT;
+      err = A.carry ? KE_CAPACITY : KE_CONFLICT;  // (a stream cannot re-run: session.cpp sizes it)
       return;
     }
     const Dewey v = dw_pin(v0);
@@ -733,9 +762,24 @@ struct Lane {
       left = refs == 0 ? 0 : refs - 1;
       nrefs = left;
       if (left == 0 && (meta >> 16) <= 1) {  // store.delete
-        if (A.defer && lk > wid) {          // a put() after this walk found the node live
-          walk_fail(KE_CONFLICT, t);
-          return false;
+        if (A.defer && lk > wid) {  // a put made after this walk was queued found the node live:
+          // in the reference the first such put throws (header); the walk itself completes
+          uint32_t i = 0;
+          for (; i < pl_n; i++) {
+            const v4u e = *PL(i);
+            if (e.x == s && e.y > wid) {
+              CEP_STAT(8);
+              if (e.y < cut_opc) {
+                cut_opc = e.y;
+                cut_ev = e.z;
+              }
+              break;
+            }
+          }
+          if (i == pl_n) {  // (a stamp without its log entry: never; re-run to be safe)
+            walk_fail(A.carry ? KE_CAPACITY : KE_CONFLICT, t);
+            return false;
+          }
         }
         del = true;
       }
@@ -855,7 +899,8 @@ struct Lane {
     bool active = false;
     for (;;) {
       if (!active) {
-        if (i >= wq_n || err) break;
+        // (walks queued after the first put a conflict makes throw never run)
+        if (i >= wq_n || err || id0 + i >= cut_opc) break;
         const v4u h = *WQ(i, 0);
         flags = (h.x >> 8) & 0xFF;
         w.n = h.x >> 24;
@@ -884,6 +929,16 @@ struct Lane {
         active = false;
       }
     }
+    if (cut_opc != CEP_NONE && !err) {  // IllegalState at that put's event: its matches dropped
+      if (wt_last == cut_ev) {
+        n_matches = wm0;
+        n_pairs = wp0;
+      }
+      err = KE_ILLEGAL_STATE;
+      err_seq = cut_ev;
+    }
+    cut_opc = CEP_NONE;
+    pl_n = 0;
     wq_n = 0;
   }
 
@@ -1071,7 +1126,7 @@ struct Lane {
     while (more) {
       CEP_PACC(8, 1);
       CEP_PT(tf0);
-      if (A.defer && __any(wq_n >= kWalkFlush)) {
+      if (A.defer && __any(wq_n >= kWalkFlush || pl_n + plog_margin() > kPutLog)) {
         flush();
         if (err) break;
       }
@@ -1120,6 +1175,8 @@ struct Lane {
     out_first = CEP_NONE;
     wq_n = 0;
     opc = 0;
+    pl_n = 0;
+    cut_opc = CEP_NONE;
     if (kCC > 0) {
       cache_invalidate();
       ev_last = CEP_NONE;
@@ -1175,6 +1232,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   Lane<F, Q> L(A, q);
   L.rb = reinterpret_cast<v4u*>(A.rings) + (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + lane;
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + lane;
+  L.pb = reinterpret_cast<v4u*>(A.plog) + (slot / 64) * ((uint64_t)kPutLog * 64) + lane;
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + lane;
   bool has = false, drained = false;
@@ -1222,7 +1280,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
     // lane has events left to run (the finished lanes' drains batched into one flush)
     const uint64_t ending = __ballot(has && phase == 1);
     CEP_PT(tf0);
-    if (A.defer && (__any(has && L.wq_n >= kWalkFlush) ||
+    if (A.defer && (__any(has && (L.wq_n >= kWalkFlush || L.pl_n + L.plog_margin() > kPutLog)) ||
                     (ending && (__popcll(ending) >= kJobDrain || !__any(has && phase == 0))))) {
       L.flush();  // every lane of the wave together (lanes without a queue leave at once)
       if (has && phase == 0 && L.err) phase = 2;  // a walk threw mid-job: the job stops there
@@ -1302,6 +1360,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   L.rb = reinterpret_cast<v4u*>(A.rings) +
          (rslot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (rslot % 64);
   L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
+  L.pb = reinterpret_cast<v4u*>(A.plog) + (slot / 64) * ((uint64_t)kPutLog * 64) + (slot % 64);
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);
   KeyState& ks = A.ks[job];

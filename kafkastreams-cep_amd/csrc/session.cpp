@@ -464,7 +464,10 @@ void run_nfa(cep_session* s, GroupRt& g) {
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
   // deferred walks a key can queue (nfa_lane.h drains at CEP_WALK_FLUSH; $CEP_WALK_CAP: tuning)
-  uint32_t wcap = 64;
+  // (a stream cannot re-run a key whose event overflows its queue: room for every walk one
+  // event can queue - removePattern and branch walks of its records, one extraction per output
+  // - beyond the drain threshold)
+  uint32_t wcap = streaming ? std::max<uint32_t>(64, 24 + 3 * rcap) : 64;
   if (const char* e = std::getenv("CEP_WALK_CAP"))
     if (std::atoi(e) > 0) wcap = (uint32_t)std::atoi(e);
   s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap));
@@ -520,6 +523,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.rcap = rcap;
   a.walks = s->walks.p;
   a.wcap = wcap;
+  a.plog = (char*)s->walks.p + putlog_off(std::max<uint64_t>(slots, 1), wcap);
   a.defer = 1;
   a.n_q = (uint32_t)Q;
   a.spread = spread;
@@ -540,8 +544,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.n_jobs = jobs;
     if (const char* e = std::getenv("CEP_JOB_MAP")) a.job_map = (uint32_t)std::atoi(e);  // (measurement runs)
   }
-  if (streaming) {  // walks in place: a conflict could not be re-run (nfa_lane.h)
-    a.defer = 0;
+  if (streaming) {  // walks deferred too: a conflict resolves exactly without a re-run (nfa_lane.h)
     a.rings = S.rings.p;
     a.nodes = S.nodes.as<Node>();
     a.preds = S.preds.as<Pred>();
@@ -684,6 +687,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));  // (may move: re-read below)
     a.rings = s->retry_rings.p;
     a.walks = s->walks.p;
+    a.plog = (char*)s->walks.p + putlog_off(std::max<uint64_t>(most, 1), wcap);
     a.order = nullptr;
     a.spread = 0;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));

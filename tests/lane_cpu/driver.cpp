@@ -14,7 +14,7 @@
 #include QUERY_SRC
 
 thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
-uint64_t cep_lane_stats[8];
+uint64_t cep_lane_stats[9];
 extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
 
 namespace {
@@ -144,12 +144,14 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       rings_batch.resize(ring_bytes(8, nslots, rc) / 16 + 64);
       scribble(rings_batch.data(), rings_batch.size() * 16);
     }
-    std::vector<v4u> walks(walkq_bytes(nslots, 64) / 16 + 64);
+    const uint32_t wc = streaming ? std::max<uint32_t>(64, 24 + 3 * rc) : 64;  // (session.cpp run_nfa)
+    std::vector<v4u> walks(walkq_bytes(nslots, wc) / 16 + 64);
     scribble(walks.data(), walks.size() * 16);
     a.rings = streaming ? g_stream.rings.data() : rings_batch.data();
     a.rcap = rc;
     a.walks = walks.data();
-    a.wcap = 64;
+    a.wcap = wc;
+    a.plog = (char*)walks.data() + putlog_offset(nslots, wc);
     a.defer = (uint32_t)df;
     blockDim.x = 256;
     for (uint64_t s = 0; s < nslots; s++) {
@@ -164,7 +166,7 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
     a.node_pool.cap = std::min<uint32_t>(a.node_pool.cap, (uint32_t)std::atol(e));
     a.pred_pool.cap = std::min<uint32_t>(a.pred_pool.cap, (uint32_t)std::atol(e));
   }
-  launch(((nk + 63) / 64) * 64 * n_q, rcap, streaming ? 0 : defer);  // session.cpp: streams walk in place
+  launch(((nk + 63) / 64) * 64 * n_q, rcap, defer);  // (session.cpp: streams defer their walks too)
   a.node_pool.cap = (uint32_t)nodes.size();
   a.pred_pool.cap = (uint32_t)preds.size();
   *n_retried = 0;
