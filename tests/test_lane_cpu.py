@@ -105,6 +105,27 @@ def test_lane_fuzz(seed):
     lane_cpu.assert_same(lane_cpu.run(ir, off, cols, defer=False), r, off)
 
 
+@pytest.mark.parametrize("seed", [21, 80, 393, 571])
+def test_lane_exact_conflicts(seed):
+    """Fuzz streams where a deferred walk deletes a node that a later put found live (the
+    reference's "Cannot find predecessor event"): resolved in the same launch through the put
+    log (nfa_lane.h header), no re-run, and equal to the oracle - per batch and streaming."""
+    import stream_split as SS
+    q = random_query(seed)
+    ir = q.to_ir()
+    off, cols = random_stream(seed, 60, 14)
+    r = oracle.run(ir, off, cols)
+    g = lane_cpu.run(ir, off, cols)
+    assert g["stats"]["exact_conflicts"] > 0 and g["retried"] == 0
+    lane_cpu.assert_same(g, r, off)
+    outs = []
+    for i, (ko, cs) in enumerate(SS.split(off, cols, 3, seed=seed)):
+        m = lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=i == 0)
+        outs.append(m)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
 @pytest.mark.parametrize("query,n_batches", [("readme", 3), ("test", 4), ("any_kleene", 3), ("strict", 5)])
 def test_lane_streaming_batches(query, n_batches):
     """A streaming session fed the stream in consecutive pieces per key produces, per key, the
