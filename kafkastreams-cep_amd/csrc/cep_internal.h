@@ -58,7 +58,6 @@ struct KeyState;
 hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap);  // double-buffered run queues
 uint64_t walkq_size(uint64_t n_slots, uint32_t wcap);        // deferred-walk queues
-uint64_t putlog_off(uint64_t n_slots, uint32_t wcap);        // their put logs' offset in that allocation
 hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list, uint32_t* conf_list,
                                 uint32_t* counts, hipStream_t st);
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,

@@ -28,7 +28,6 @@ struct NfaArgs {
   uint32_t rcap;
   void* walks;               // deferred-walk queues, wcap per slot (nfa_lane.h)
   uint32_t wcap;
-  void* plog;                // the walk queues' put logs (nfa_lane.h kPutLog per slot, in `walks`)
   uint32_t defer;            // 1: queue buffer walks and drain them wave-wide; 0: walk in place
   // Jobs: a job is (query qi of the launch, key), id qi * n_keys + key.  Without a job list, job
   // index i is query i % n_q on the key of rank i / n_q, rank -> key through `order` (lane

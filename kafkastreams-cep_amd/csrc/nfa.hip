@@ -553,7 +553,6 @@ hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_le
 }
 
 uint64_t walkq_size(uint64_t n_slots, uint32_t wcap) { return walkq_bytes(n_slots, wcap); }
-uint64_t putlog_off(uint64_t n_slots, uint32_t wcap) { return putlog_offset(n_slots, wcap); }
 
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap) {
   return ring_bytes(F <= 2 ? 2 : (F <= 4 ? 4 : 8), n_slots, rcap);

@@ -128,9 +128,16 @@ constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the 
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
-// put-log entries per lane ({node, walks queued, event, -}), after the walk queues in A.walks;
-// the wave drains its walks before an event could overflow it
+// put-log entries per lane ({node, walks queued, event, -}), after each 64 lanes' walk queues
+// in A.walks (the log's address is the walk queue's plus a launch constant); the wave drains
+// its walks before an event could overflow it
 constexpr uint32_t kPutLog = 256;
+// The narrow build of a query (compile.cpp) leaves the put log out - the registers it costs
+// spill there - and reports a conflict as KE_CONFLICT: the key is re-run in the wide build,
+// which resolves it.  (Default: on.)
+#ifndef CEP_PUT_LOG
+#define CEP_PUT_LOG 1
+#endif
 // a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
 // re-runs the job in the wide one (a retry); the wide build's limit is final
 constexpr int32_t kDwFull = kDeweyPairs < 6 ? KE_RETRY : KE_CAPACITY;
@@ -187,14 +194,12 @@ __host__ __device__ inline uint64_t ring_bytes(int F, uint64_t n_slots, uint32_t
   return ((n_slots + 63) / 64) * 64ull * 2ull * rcap * quads * 16ull;
 }
 
-// bytes of deferred-walk queues for n_slots lanes of wcap walks, then their put logs
+// bytes of deferred-walk queues for n_slots lanes of wcap walks and their put logs
 __host__ __device__ inline uint64_t walkq_bytes(uint64_t n_slots, uint32_t wcap) {
   return ((n_slots + 63) / 64) * 64ull * (wcap * kWalkQuads + kPutLog) * 16ull;
 }
-// the put logs' offset in that allocation
-__host__ __device__ inline uint64_t putlog_offset(uint64_t n_slots, uint32_t wcap) {
-  return ((n_slots + 63) / 64) * 64ull * wcap * kWalkQuads * 16ull;
-}
+// quads per 64 lanes of that allocation
+__host__ __device__ inline uint64_t walkq_group_quads(uint32_t wcap) { return (wcap * (uint64_t)kWalkQuads + kPutLog) * 64; }
 
 template <int F, class Q>
 struct Lane {
@@ -213,8 +218,7 @@ struct Lane {
   uint32_t ev_pos = CEP_NONE;
   v4u* rb;  // this lane's quad 0 of half 0, slot 0 (stride 64 quads)
   lds_v4u* lr;  // LDS slots: this lane's quad 0 of half 0, slot 0 (stride 64 quads)
-  v4u* wb;  // this lane's walk queue, slot 0 quad 0 (stride 64 quads)
-  v4u* pb;  // this lane's put log, entry 0 (stride 64 quads)
+  v4u* wb;  // this lane's walk queue, slot 0 quad 0 (stride 64 quads), then its put log
   uint32_t half = 0, count = 0, ocount = 0;  // input half, its records, records written
   uint32_t bdig = 1;                         // kBeginReg: the begin run's version "bdig"
   uint32_t n_final = 0;                      // finals queued at this event
@@ -233,7 +237,6 @@ struct Lane {
   uint32_t wq_n = 0;  // queued
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
   uint32_t pl_n = 0;  // put-log entries since the last flush
-  uint32_t cut_opc = CEP_NONE, cut_ev = 0;  // the first put that a queued walk's delete makes throw
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
 #ifdef CEP_PROF
   unsigned long long prof[14] = {};  // the time split (see CEP_PROF above), this wave / lane
@@ -257,7 +260,7 @@ struct Lane {
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
   }
-  __device__ __forceinline__ v4u* PL(uint32_t i) const { return pb + (uint64_t)i * 64; }
+  __device__ __forceinline__ v4u* PL(uint32_t i) const { return wb + ((uint64_t)A.wcap * kWalkQuads + i) * 64; }
   // put-log entries one event may add at most (its records' puts): the wave drains before
   __device__ __forceinline__ uint32_t plog_margin() const {
     return 2 * A.rcap + 4 < kPutLog / 2 ? 2 * A.rcap + 4 : kPutLog / 2;
@@ -526,6 +529,7 @@ struct Lane {
       err = KE_ILLEGAL_STATE;
       return CEP_NONE;
     }
+#if CEP_PUT_LOG
     if (A.defer && wq_n > 0) {  // found live while walks are queued: stamp and log (conflict check)
       if (pl_n >= kPutLog) {        // (only an event with more puts than plog_margin())
         err = A.carry ? KE_CAPACITY : KE_CONFLICT;
@@ -534,6 +538,9 @@ struct Lane {
       A.nodes[p].lk = opc;
       *PL(pl_n++) = v4u{p, opc, j, 0u};
     }
+#else
+    if (A.defer) A.nodes[p].lk = opc;  // found live after `opc` queued walks (conflict check)
+#endif
     const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
     if (c == CEP_NONE) return new_node(sk, p, v);
     append_pred(c, p, v);
@@ -735,8 +742,18 @@ struct Lane {
   // (Prefetching the next node ahead of this step's stores was measured: 4 % on the heavy
   // walk bench, but 16 more live VGPRs across the drain loop cost cfg 3's kernel 11 % in
   // spills; the step loads its own node.)
+  // the put-log entry of the first put after walk `wid` that found node `s` live (CEP_NONE: none)
+  __device__ __forceinline__ uint32_t first_put_after(uint32_t s, uint32_t wid) const {
+    for (uint32_t i = 0; i < pl_n; i++) {
+      const v4u e = *PL(i);
+      if (e.x == s && e.y > wid) return i;
+    }
+    return CEP_NONE;
+  }
+
+  // `conf` (deferred walks): set to the node when its delete conflicts with a later put
   __device__ __forceinline__ bool walk_node(uint32_t flags, uint32_t& s, Dewey& w, uint32_t t, uint32_t wid,
-                                            uint32_t& np) {
+                                            uint32_t& np, uint32_t& conf) {
     if (s == CEP_NONE) {
       walk_fail(KE_NPE, t);
       return false;
@@ -763,23 +780,14 @@ struct Lane {
       nrefs = left;
       if (left == 0 && (meta >> 16) <= 1) {  // store.delete
         if (A.defer && lk > wid) {  // a put made after this walk was queued found the node live:
-          // in the reference the first such put throws (header); the walk itself completes
-          uint32_t i = 0;
-          for (; i < pl_n; i++) {
-            const v4u e = *PL(i);
-            if (e.x == s && e.y > wid) {
-              CEP_STAT(8);
-              if (e.y < cut_opc) {
-                cut_opc = e.y;
-                cut_ev = e.z;
-              }
-              break;
-            }
-          }
-          if (i == pl_n) {  // (a stamp without its log entry: never; re-run to be safe)
-            walk_fail(A.carry ? KE_CAPACITY : KE_CONFLICT, t);
-            return false;
-          }
+#if CEP_PUT_LOG
+          // in the reference the first such put throws (header); the walk itself completes, the
+          // drain loop finds that put (fewer live registers there than in the step)
+          conf = s;
+#else
+          walk_fail(KE_CONFLICT, t);  // (the narrow build: the key is re-run in the wide one)
+          return false;
+#endif
         }
         del = true;
       }
@@ -878,7 +886,8 @@ struct Lane {
     uint64_t npa = 0;
     if (!walk_start(flags, sk, ev, first, t, s, npa, np)) return;
     Dewey w = dw_pin(v);
-    while (walk_node(flags, s, w, t, 0, np)) {
+    uint32_t conf = CEP_NONE;  // (in place: no conflicts)
+    while (walk_node(flags, s, w, t, 0, np, conf)) {
     }
     if (!err) walk_end(flags, npa, np);
   }
@@ -897,10 +906,12 @@ struct Lane {
     Dewey w;
     dw_init(w, 0);
     bool active = false;
+    uint32_t cut = CEP_NONE;   // put-log entry of the first put a walk's delete makes throw
+    uint32_t conf = CEP_NONE;  // the node of this step's conflicting delete
     for (;;) {
       if (!active) {
         // (walks queued after the first put a conflict makes throw never run)
-        if (i >= wq_n || err || id0 + i >= cut_opc) break;
+        if (i >= wq_n || err || (cut != CEP_NONE && id0 + i >= PL(cut)->y)) break;
         const v4u h = *WQ(i, 0);
         flags = (h.x >> 8) & 0xFF;
         w.n = h.x >> 24;
@@ -923,21 +934,32 @@ struct Lane {
         active = true;
       }
       CEP_STAT(7);
-      if (!walk_node(flags, s, w, t, id0 + i - 1, np)) {
+      const bool more = walk_node(flags, s, w, t, id0 + i - 1, np, conf);
+      if (conf != CEP_NONE) {
+        const uint32_t k = first_put_after(conf, id0 + i - 1);
+        conf = CEP_NONE;
+        if (k == CEP_NONE) {  // (a stamp without its log entry: never; re-run to be safe)
+          walk_fail(A.carry ? KE_CAPACITY : KE_CONFLICT, t);
+          break;
+        }
+        CEP_STAT(8);
+        if (cut == CEP_NONE || PL(k)->y < PL(cut)->y) cut = k;  // (the earliest such put)
+      }
+      if (!more) {
         if (err) break;
         walk_end(flags, npa, np);
         active = false;
       }
     }
-    if (cut_opc != CEP_NONE && !err) {  // IllegalState at that put's event: its matches dropped
-      if (wt_last == cut_ev) {
+    if (cut != CEP_NONE && !err) {  // IllegalState at that put's event: its matches dropped
+      const uint32_t ce = PL(cut)->z;
+      if (wt_last == ce) {
         n_matches = wm0;
         n_pairs = wp0;
       }
       err = KE_ILLEGAL_STATE;
-      err_seq = cut_ev;
+      err_seq = ce;
     }
-    cut_opc = CEP_NONE;
     pl_n = 0;
     wq_n = 0;
   }
@@ -1176,7 +1198,6 @@ struct Lane {
     wq_n = 0;
     opc = 0;
     pl_n = 0;
-    cut_opc = CEP_NONE;
     if (kCC > 0) {
       cache_invalidate();
       ev_last = CEP_NONE;
@@ -1231,8 +1252,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   const uint32_t lane = threadIdx.x & 63;
   Lane<F, Q> L(A, q);
   L.rb = reinterpret_cast<v4u*>(A.rings) + (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + lane;
-  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + lane;
-  L.pb = reinterpret_cast<v4u*>(A.plog) + (slot / 64) * ((uint64_t)kPutLog * 64) + lane;
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap) + lane;
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + lane;
   bool has = false, drained = false;
@@ -1359,8 +1379,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   const uint64_t rslot = A.carry ? job : slot;
   L.rb = reinterpret_cast<v4u*>(A.rings) +
          (rslot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (rslot % 64);
-  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * ((uint64_t)A.wcap * kWalkQuads * 64) + (slot % 64);
-  L.pb = reinterpret_cast<v4u*>(A.plog) + (slot / 64) * ((uint64_t)kPutLog * 64) + (slot % 64);
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap) + (slot % 64);
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);
   KeyState& ks = A.ks[job];

@@ -523,7 +523,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.rcap = rcap;
   a.walks = s->walks.p;
   a.wcap = wcap;
-  a.plog = (char*)s->walks.p + putlog_off(std::max<uint64_t>(slots, 1), wcap);
   a.defer = 1;
   a.n_q = (uint32_t)Q;
   a.spread = spread;
@@ -634,7 +633,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   }
 
   // Re-run the jobs that hit a capacity limit (with 8x the run queue and 4x every exhausted
-  // pool; walks still deferred) and those whose deferred walks conflicted (walks in place),
+  // pool; walks still deferred) and those whose deferred walks conflicted,
   // in the wide Dewey build (a narrow-build job whose version outgrew 3 pairs is a capacity
   // re-run too).
   // The job lists are collected on the device; only their lengths come back.
@@ -687,13 +686,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
     s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));  // (may move: re-read below)
     a.rings = s->retry_rings.p;
     a.walks = s->walks.p;
-    a.plog = (char*)s->walks.p + putlog_off(std::max<uint64_t>(most, 1), wcap);
     a.order = nullptr;
     a.spread = 0;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
-    for (int k = 0; k < 2; k++) {  // capacity re-runs keep deferred walks, conflicts walk in place
+    // capacity re-runs keep deferred walks; conflicts too (the wide build resolves them
+    // exactly through its put log, nfa_lane.h), except after a put log overflowed: in place
+    for (int k = 0; k < 2; k++) {
       if (!lens[k]) continue;
-      a.defer = k == 0 ? 1 : 0;
+      a.defer = (k == 0 || round == 0) ? 1 : 0;
       a.jobs = k == 0 ? cap_list : conf_list;
       a.n_jobs = lens[k];
       a.job_next = &sc->job_next;  // re-runs always on persistent lanes

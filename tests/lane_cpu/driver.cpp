@@ -151,7 +151,6 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
     a.rcap = rc;
     a.walks = walks.data();
     a.wcap = wc;
-    a.plog = (char*)walks.data() + putlog_offset(nslots, wc);
     a.defer = (uint32_t)df;
     blockDim.x = 256;
     for (uint64_t s = 0; s < nslots; s++) {
