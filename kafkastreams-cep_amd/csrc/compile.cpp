@@ -550,7 +550,10 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // a single query's narrow build never runs persistent lanes (session.cpp: only kernel groups
   // and the re-runs, which take the wide build, do): its kernel holds run() alone, half the code
   if (!lits.param) o += "#ifndef CEP_PERSIST_LANES\n#define CEP_PERSIST_LANES 0\n#endif\n";
-  o += "#endif\n";
+  o += "#define CEP_WAVES_EU 3\n#endif\n";
+  // the wide build (6-pair Dewey versions: streams, re-runs) at 2 waves per SIMD: at 3 it
+  // spills ~200 B of scratch and ran 20-25 % slower (profiles/r03)
+  o += "#ifndef CEP_WAVES_EU\n#define CEP_WAVES_EU 2\n#endif\n";
   o += "#include <hip/hip_runtime.h>\n#include <stdint.h>\n#include \"cep_layout.h\"\n#include \"kernel_args.h\"\n";
   if (lits.param) o += "#define CEP_WALK_COMPAT2 1  // kernel group: the wider straight-line walk step\n";
   o += "#include \"dewey.h\"\n#include \"java.h\"\n#include \"nfa_lane.h\"\n\nnamespace cep {\nnamespace {\n\n";
@@ -838,12 +841,14 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "      Dewey v = c.ver;\n      if (o.produced > 0 && !dw_add_run(v)) { L.err = kDwFull; return -1; }\n";
   o += "      if (!L.readd_begin(c.stage & 0xFF, v)) return -1;\n";
   o += "      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
-  // Occupancy: at least 3 waves per SIMD (<= 168 VGPRs; measured best: 2 waves lose ~20 %,
-  // 4+ spill to scratch).  $CEP_JIT_WAVES overrides for tuning runs (0: compiler's choice).
-  int waves = 3;
-  if (const char* wv = std::getenv("CEP_JIT_WAVES")) waves = std::atoi(wv);
-  std::string occ;
-  if (waves > 0) occ = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))";
+  // Occupancy: the narrow build at 3 waves per SIMD (<= 168 VGPRs; measured best: 2 waves
+  // lose ~20 %, 4+ spill to scratch), the wide one at 2 (CEP_WAVES_EU above).
+  // $CEP_JIT_WAVES overrides both for tuning runs (0: compiler's choice).
+  std::string occ = " __attribute__((amdgpu_waves_per_eu(CEP_WAVES_EU)))";
+  if (const char* wv = std::getenv("CEP_JIT_WAVES")) {
+    const int waves = std::atoi(wv);
+    occ = waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : "";
+  }
   o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256)" + occ + " cep_nfa_jit(NfaArgs A) {\n";
   o += "  JitQ q(A);\n";
   o += "  __shared__ v4u ring_lds[JitQ::kRingLds > 0 ? 4 * 2 * JitQ::kRingLds * RecLayout<F, JitQ::kFold32>::kLdsQuads * 64 : 1];\n";

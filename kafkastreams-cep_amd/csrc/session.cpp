@@ -408,11 +408,15 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // Per-batch sessions run persistent lanes (nfa_lane.h run_jobs): a grid of about what the
   // chip holds at once (3 waves per SIMD), every lane claiming job after job.  Streams keep one
   // lane per key (their run queues live at the key's slot).
-  uint64_t waves_cu = 12;  // 3 per SIMD (the JIT kernel's occupancy); $CEP_RESIDENT_WAVES (per CU): measurement runs
+  // waves per CU of the JIT kernels (compile.cpp): the narrow build 3 per SIMD, the wide one
+  // (streams, re-runs) 2; $CEP_RESIDENT_WAVES (per CU): measurement runs
+  uint64_t waves_cu = streaming ? 8 : 12, waves_cu_wide = 8;
   if (const char* e = std::getenv("CEP_RESIDENT_WAVES"))
-    if (std::atoi(e) > 0) waves_cu = (uint64_t)std::atoi(e);
+    if (std::atoi(e) > 0) waves_cu = waves_cu_wide = (uint64_t)std::atoi(e);
   const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
+  const uint64_t resident_wide = (uint64_t)s->cus * waves_cu_wide * 64;
   auto grid_for = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident); };
+  auto grid_wide = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident_wide); };
   // $CEP_NO_PERSIST (measurement runs): one lane per job.  Single queries run one lane per key:
   // their longest-first lane order already balances the waves (persistent lanes cost cfg 3
   // ~35 %), and their narrow kernel is built without the persistent driver; groups mix light
@@ -679,7 +683,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.out_pool.cap = (uint32_t)out_cap;
     // a bigger run queue per retried job, its ring kept within 16 GiB
     rcap *= 8;
-    const uint64_t most = grid_for(std::max<uint64_t>(lens[0], lens[1]));
+    // (re-runs take the wide build: its occupancy; the interpreter tier keeps the default)
+    auto grid_re = [&](uint64_t n) { return g.fn ? grid_wide(n) : grid_for(n); };
+    const uint64_t most = grid_re(std::max<uint64_t>(lens[0], lens[1]));
     while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
     a.rcap = rcap;
     s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
@@ -698,7 +704,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
       a.n_jobs = lens[k];
       a.job_next = &sc->job_next;  // re-runs always on persistent lanes
       HIPCHECK(hipMemsetAsync(&sc->job_next, 0, sizeof(uint32_t), s->stream));
-      HIPCHECK(launch_nfa_tier(g, r0.q, a, grid_for(lens[k]), s->stream, true));
+      HIPCHECK(launch_nfa_tier(g, r0.q, a, grid_re(lens[k]), s->stream, true));
       launches++;
       g.stats.retried_jobs += lens[k];
     }

@@ -30,7 +30,7 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False):
     library (cached).  The wide Dewey build (6 pairs) unless `narrow`: the driver re-runs jobs
     in the same build, while libcep re-runs the narrow build's overflowing jobs in the wide one."""
     # the occupancy attribute is for the GPU compile only (the host has no kernels)
-    src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\d+\)\)\)", "", source or N.Query(ir).jit_source)
+    src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\w+\)\)\)", "", source or N.Query(ir).jit_source)
     if not narrow:
         src = "#define CEP_DEWEY_PAIRS 6\n" + src
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
