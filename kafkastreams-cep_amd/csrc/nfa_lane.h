@@ -539,7 +539,9 @@ struct Lane {
       *PL(pl_n++) = v4u{p, opc, j, 0u};
     }
 #else
-    if (A.defer) A.nodes[p].lk = opc;  // found live after `opc` queued walks (conflict check)
+    // found live after `opc` queued walks (conflict check; only a walk queued before this put
+    // can conflict with it: none is when the queue is empty)
+    if (A.defer && wq_n > 0) A.nodes[p].lk = opc;
 #endif
     const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
     if (c == CEP_NONE) return new_node(sk, p, v);
