@@ -21,7 +21,9 @@
 #include <hip/hip_runtime.h>
 
 #include "cep_layout.h"
-#include "nfa_device.h"
+#include "dewey.h"
+#include "interp.h"
+#include "java.h"
 #include "nfa_lane.h"
 
 namespace cep {

@@ -26,7 +26,9 @@
 #include <type_traits>
 
 #include "cep_layout.h"
-#include "nfa_device.h"
+#include "dewey.h"
+#include "interp.h"
+#include "java.h"
 #include "stencil_args.h"
 
 namespace cep {
