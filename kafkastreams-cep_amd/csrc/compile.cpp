@@ -533,7 +533,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
   // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_EST_MODE"})
+  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:
@@ -873,23 +873,17 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n  const uint32_t lane = threadIdx.x & 63;\n";
     o += "  if (k >= A.n_keys) return;\n";
     o += "  const uint64_t base = A.key_off[k];\n  const uint32_t n = (uint32_t)(A.key_off[k + 1] - base);\n";
-    o += "  uint64_t w = 0;\n  uint32_t first = n;  // the first begin hit (its position)\n";
+    o += "  uint64_t w = 0;\n";
     o += "  const uint64_t p1 = base + n;\n";
     o += "  for (uint64_t wi = (base >> 6) + lane; n > 0 && wi <= ((p1 - 1) >> 6); wi += 64) {\n";
     o += "    uint64_t bits = A.bhits[wi];\n    const uint64_t s = wi << 6;\n";
     o += "    if (s < base) bits &= ~0ull << (base - s);\n";
     o += "    if (p1 - s < 64) bits &= (1ull << (p1 - s)) - 1ull;\n";
     o += "    while (bits) {\n      const uint32_t b = (uint32_t)__builtin_ctzll(bits);\n      bits &= bits - 1ull;\n";
-    o += "      if (first == n) first = (uint32_t)(s + b - base);\n";
     o += "      w += n - (uint32_t)(s + b - base);\n    }\n  }\n";
-    o += "  for (int o = 32; o > 0; o >>= 1) {\n    w += __shfl_down(w, o, 64);\n";
-    o += "    const uint32_t f = __shfl_down(first, o, 64);\n    first = f < first ? f : first;\n  }\n";
-    // ($CEP_EST_MODE, measurement runs: 1 = the events stepped after the first begin hit, 2 =
-    // that span first, then the mean live runs over it)
-    o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n  w = n - first;\n";
-    o += "#elif defined(CEP_EST_MODE) && CEP_EST_MODE == 2\n";
-    o += "  { const uint64_t span = n - first; const uint64_t r = span ? (w * 16) / span : 0;\n";
-    o += "    w = (span << 8) | (r < 255 ? r : 255); }\n#endif\n";
+    // (ordering by the span after the first begin hit instead, or by span then mean live
+    // runs, was measured: cfg 3 31.5 -> 34.1 / 33.2 ms)
+    o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n";
