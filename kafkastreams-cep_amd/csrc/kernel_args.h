@@ -40,6 +40,7 @@ struct NfaArgs {
                              // null: one job per lane (streaming sessions)
   uint64_t spread;           // W > 0: an underfilled single-query launch of W waves, wave w's lane l
                              // running rank l * W + w (session.cpp run_nfa); 0: rank w * 64 + l
+  uint32_t spread_snake;     // spread: odd lanes take their row of ranks in reverse
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)

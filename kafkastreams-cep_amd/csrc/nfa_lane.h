@@ -1365,8 +1365,12 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   } else {
     const uint32_t nq = A.n_q ? A.n_q : 1;
     const uint64_t w = slot / 64;
-    // spread: the heaviest W keys (lane order) lead one wave each, the next W are their lanes 1, ...
-    const uint64_t rank = A.spread ? (slot % 64) * A.spread + w : (w / nq) * 64 + slot % 64;
+    // spread: the heaviest W keys (lane order) lead one wave each, the next W are their lanes 1,
+    // ...; spread_snake: odd lanes take their row in reverse (wave 0's lane 1 is the row's
+    // lightest key), so the waves of the heaviest keys carry the lightest neighbours
+    const uint64_t l = slot % 64;
+    const uint64_t rank = A.spread ? l * A.spread + ((A.spread_snake && (l & 1)) ? A.spread - 1 - w : w)
+                                   : (w / nq) * 64 + l;
     if (rank >= A.n_keys) return;
     job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
   }

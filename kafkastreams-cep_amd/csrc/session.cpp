@@ -428,9 +428,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // divergent lanes.  So its keys are spread over every wave slot the chip holds: the heaviest
   // keys lead one wave each, with lighter keys beside them ($CEP_SPREAD=0: measurement runs).
   uint64_t spread = 0;
+  // (odd lanes take their row of ranks reversed: the slowest world-8 shard 16.5 -> 15.6 ms;
+  // $CEP_SPREAD: 0 off, 1 rows in order, 2 (default) odd lanes reversed - measurement runs)
+  uint32_t snake = 0;
   if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64) {
     const char* e = std::getenv("CEP_SPREAD");
-    if (!e || std::atoi(e) != 0) spread = std::min<uint64_t>(resident / 64, nk);
+    const int mode = e ? std::atoi(e) : 2;
+    if (mode != 0) spread = std::min<uint64_t>(resident / 64, nk);
+    snake = mode == 2 ? 1u : 0u;
   }
   const uint64_t slots = spread ? spread * 64 : !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
@@ -530,6 +535,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.defer = 1;
   a.n_q = (uint32_t)Q;
   a.spread = spread;
+  a.spread_snake = snake;
   a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
   a.preds = s->preds.as<Pred>();

@@ -48,7 +48,7 @@ def main():
     for r in ranks:
         keys, loff = SH.shard_layout(off, args.world, r)
         sh, _ = N.shard_stream(stream, keys, loff)
-        for sp in ("0", "1"):
+        for sp in os.environ.get("SPREAD_MODES", "0,1").split(","):
             os.environ["CEP_SPREAD"] = sp
             wall, main_ms, dig = timed(s, sh, args.steps)
             print(json.dumps({"rank": r, "spread": sp, "keys": int(len(keys)), "wall_ms": wall, "main_ms": main_ms,
