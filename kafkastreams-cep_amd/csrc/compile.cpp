@@ -362,6 +362,10 @@ struct Gen {
   LitCtx* L = nullptr;
   std::string fail;   // statement tail after `err = X;` (e.g. "return false;")
   int aggType = 0;    // state type of `curr` inside an aggregator
+  // a matcher already evaluated without an exception on the same event and state (the
+  // stage's edge-0 predicate, evaluated first by matchEdgesAndGet): its value is `knownName`
+  const M* known = nullptr;
+  std::string knownName;
   std::string t() { return "t" + std::to_string(n++); }
   void raise(const char* code, const std::string& cond) { s += "  if (" + cond + ") { err = " + code + "; " + fail + " }\n"; }
 
@@ -482,6 +486,7 @@ struct Gen {
     return r.first;
   }
   std::string matcher(const M* m) {
+    if (known && m == known) return knownName;
     switch (m->k) {
       case M::TRUE_: return "true";
       case M::LEAF: return operand(m->leaf);
@@ -586,17 +591,31 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // predicates, one per (stage, edge); folds one per (stage, aggregate)
   std::string pa;
   std::vector<std::vector<std::string>> predName(d.n_stages, std::vector<std::string>(3));
+  // The later edges of a stage (IGNORE = !pred, PROCEED = succ || (!pred && !ignore)) embed the
+  // edge-0 predicate itself; matchEdgesAndGet (NFA.java:267-273) evaluates edge 0 first, so
+  // by then it returned without an exception and its value on the same event and state is m0:
+  // those predicates take it as an argument instead of evaluating it again.
+  std::vector<std::vector<bool>> predM0(d.n_stages, std::vector<bool>(3, false));
+  std::vector<const M*> edge0(d.n_stages, nullptr);
+  for (auto& pe : b.pending)
+    if (pe.edge == 0 && pe.m->k != M::TRUE_) edge0[pe.stage] = pe.m.get();
   for (auto& pe : b.pending) {
     if (pe.m->k == M::TRUE_) { predName[pe.stage][pe.edge] = ""; continue; }
     Gen g;
     g.L = &lits;
     g.stateType = stTypes;
     g.fail = "return false;";
+    const bool m0 = pe.edge > 0 && edge0[pe.stage] != nullptr;
+    if (m0) {
+      g.known = edge0[pe.stage];
+      g.knownName = "m0";
+    }
     const std::string v = g.matcher(pe.m.get());
     const std::string name = "P" + std::to_string(pe.stage) + "_" + std::to_string(pe.edge);
     predName[pe.stage][pe.edge] = name;
-    pa += "__device__ __forceinline__ bool " + name + "(const Ev& ev, const Fo& w, int& err, const Kc& K) {\n" + g.s +
-          "  (void)K;\n  return " + v + ";\n}\n";
+    predM0[pe.stage][pe.edge] = m0;
+    pa += "__device__ __forceinline__ bool " + name + "(const Ev& ev, const Fo& w, int& err, const Kc& K" +
+          (m0 ? ", bool m0" : "") + ") {\n" + g.s + "  (void)K;\n  return " + v + ";\n}\n";
   }
   std::vector<std::vector<std::string>> aggName(d.n_stages);
   for (auto& sa : b.stageAggs) {
@@ -704,7 +723,8 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     f += "    int err = 0;\n";
     for (int e = 0; e < S.n_edges; e++) {  // matchEdgesAndGet: every predicate first, in order
       const std::string& pn = predName[s][e];
-      f += "    const bool m" + std::to_string(e) + " = " + (pn.empty() ? std::string("true") : pn + "(ev, w, err, K)") + ";\n";
+      f += "    const bool m" + std::to_string(e) + " = " +
+           (pn.empty() ? std::string("true") : pn + "(ev, w, err, K" + (predM0[s][e] ? ", m0" : "") + ")") + ";\n";
       if (!pn.empty()) f += "    if (err) { L.err = err; return; }\n";
     }
     std::string hasT = "false", hasP = "false", hasI = "false", hasB = "false";
