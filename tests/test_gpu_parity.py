@@ -160,6 +160,45 @@ def test_cfg3_stock_small(variant, tier):
     assert_parity(gpu_run(ir, off, cols, tier=tier), r, off)
 
 
+def test_cfg3_medium_bit_exact():
+    """Config 3 at 50k keys (every 20th key of the BASELINE stream, 50M events): every match,
+    event id, emission order and exception bit-exact against the oracle - a launch the size of
+    an 8-GPU shard's third, so the spread lane mapping (session.cpp, underfilled launches) and
+    the narrow build's re-runs run at scale."""
+    cfg = W.CONFIGS[3]
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 20))
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=16)
+    assert r["n_matches"] > 30000
+    assert_parity(gpu_run(ir, off, cols), r, off)
+
+
+def test_cfg4_stress_medium_bit_exact():
+    """Config 4's stress variant at 20k keys (20M events, ~200 buffer nodes per key)."""
+    cfg = W.CONFIGS[3]
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 50))
+    ir = W.any_kleene_query(carry_volume=True).to_ir()
+    r = oracle.run(ir, off, cols, threads=16)
+    assert r["n_matches"] > 10000 and int(np.count_nonzero(r["err_code"])) == 0
+    assert_parity(gpu_run(ir, off, cols), r, off)
+
+
+def test_cfg5_medium_bit_exact():
+    """Config 5's 64-variant kernel group on 2000 keys of the BASELINE stream (2M events x 64
+    queries): every query bit-exact against the oracle."""
+    cfg = W.CONFIGS[3]
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 500))
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)]
+    s = N.Session(qs)
+    s.push(off, cols)
+    total = 0
+    for i, q in enumerate(qs):
+        r = oracle.run(q.ir, off, cols, threads=16)
+        total += r["n_matches"]
+        assert_parity(session_result(s, i, off), r, off)
+    assert total > 50000
+
+
 @pytest.mark.parametrize("tier", TIERS)
 def test_cfg4_any_kleene_small(tier):
     cfg = W.SynthConfig("t", "stock", 400, 300, 0xCE90000 + 4)
