@@ -817,7 +817,8 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     }
     if (q->windowed) f += "      fv[FS] = w.v[FS];  // the branch keeps the run's start\n      fv[FS + 1] = w.v[FS + 1];\n";
     f += "      L.set_folds(r, fv, nm);\n      o.produced++;\n";
-    f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver);\n      if (L.err) return;\n    }\n";
+    f += "      L.walk_branch(prev_sk, top.event, top.ev_first, ver, prev_sk == top.hsk ? top.node : CEP_NONE);\n"
+         "      if (L.err) return;\n    }\n";
     if (S.n_aggs) {
       f += "    if (consumed) {\n";
       for (auto& an : aggName[s]) f += "      " + an + "(ev, w, err, K);\n      if (err) { L.err = err; return; }\n";

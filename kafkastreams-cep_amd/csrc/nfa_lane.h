@@ -128,6 +128,12 @@ constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the 
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
+// the entry's `first` field holds the walk's start node itself (the record's node hint, live
+// when the walk was queued - an epsilon record's hint is its node of (stage key, event)): no
+// lookup at the walk's start.  Exact: no node is taken from the pool during a flush, so a
+// start node deleted by an earlier walk of the flush is found dead (NPE) by walk_node, as the
+// lookup would find none.
+constexpr uint32_t kWalkHint = 8;
 // put-log entries per lane ({node, walks queued, event, -}), after each 64 lanes' walk queues
 // in A.walks (the log's address is the walk queue's plus a launch constant); the wave drains
 // its walks before an event could overflow it
@@ -673,11 +679,16 @@ struct Lane {
   // ---------------------------------------------------------------- walks
   // branch  KVSharedVersionedBuffer.java:99-110;  peek(remove=true)  :143-171 (emit: the
   // match construction's Sequence).  In place when !A.defer, else queued (see the header).
-  __device__ __forceinline__ void walk(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v0) {
+  __device__ __forceinline__ void walk(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v0,
+                                      uint32_t hint = CEP_NONE) {
     CEP_STAT(2);
-    if (!A.defer) {
+    if (!A.defer) {  // (in place: hints are not kept valid)
       walk_now(flags, sk, ev, first, v0, j);
       return;
+    }
+    if (hint != CEP_NONE) {
+      flags |= kWalkHint;
+      first = hint;
     }
     if (wq_n >= A.wcap) {  // more walks in one event than the queue holds: re-run in place
       err = A.carry ? KE_CAPACITY : KE_CONFLICT;  // (a stream cannot re-run: session.cpp sizes it)
@@ -695,11 +706,14 @@ struct Lane {
     wq_n++;
     opc++;
   }
-  __device__ __forceinline__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v) {
-    walk(kWalkBranch, sk, ev, first, v);
+  // `hint`: the node (sk, ev) when the caller knows it (a record's node hint), else CEP_NONE
+  __device__ __forceinline__ void walk_branch(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v,
+                                             uint32_t hint = CEP_NONE) {
+    walk(kWalkBranch, sk, ev, first, v, hint);
   }
-  __device__ __forceinline__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit) {
-    walk(emit ? kWalkEmit : 0u, sk, ev, first, v);
+  __device__ __forceinline__ void walk_remove(uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v, bool emit,
+                                             uint32_t hint = CEP_NONE) {
+    walk(emit ? kWalkEmit : 0u, sk, ev, first, v, hint);
   }
 
   // a walk of event t threw: nothing of event t is forwarded, the key stops at t
@@ -861,7 +875,7 @@ struct Lane {
       walk_fail(KE_NPE, t);
       return false;
     }
-    s = lookup(sk, first);
+    s = (flags & kWalkHint) ? first : lookup(sk, first);
     np = 0;
     if (flags & kWalkEmit) {
       out_put(t);
@@ -995,7 +1009,7 @@ struct Lane {
       if (err) return;
       CEP_PACC(9, 1);
       if (produced == 0) {  // removePattern
-        walk_remove(q.stage_sk(c.stage), c.event, c.ev_first, c.ver, false);
+        walk_remove(q.stage_sk(c.stage), c.event, c.ev_first, c.ver, false, (c.stage & kRecEps) ? c.node : CEP_NONE);
         if (err) return;
       }
     }
@@ -1041,7 +1055,7 @@ struct Lane {
       if (hd.x & kRecFinal) {
         Rec<F> r;
         load(oh, i, r, cur_first);
-        walk_remove(q.stage_sk(r.stage), r.event, r.ev_first, r.ver, true);
+        walk_remove(q.stage_sk(r.stage), r.event, r.ev_first, r.ver, true, (r.stage & kRecEps) ? r.node : CEP_NONE);
         if (err) return;
       } else {
         if (w != i) copy_rec(oh, i, w);
