@@ -1241,6 +1241,14 @@ struct Lane {
 __device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
   if (A.jobs) return A.jobs[idx];
   const uint32_t nq = A.n_q ? A.n_q : 1;
+  if (A.qmap) {  // heavy-first: the heavy queries' jobs over all ranks, then the light ones'
+    const uint64_t nh = (uint64_t)A.n_heavy * A.n_keys;
+    const uint64_t i = idx < nh ? idx : idx - nh;
+    const uint32_t np = idx < nh ? A.n_heavy : nq - A.n_heavy;
+    const uint64_t rank = i / np;
+    const uint32_t qi = A.qmap[(idx < nh ? 0u : A.n_heavy) + (uint32_t)(i % np)];
+    return (uint64_t)qi * A.n_keys + (A.order ? A.order[rank] : rank);
+  }
   uint64_t rank = idx / nq;
   uint32_t qi = (uint32_t)(idx % nq);
   if (A.job_map == 1 && nq % 8 == 0) {

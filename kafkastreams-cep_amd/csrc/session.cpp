@@ -193,6 +193,11 @@ struct GroupRt {
   // pool use of the last batch (the next batch's pools are sized from it)
   uint64_t last_nodes = 0, last_preds = 0, last_out = 0;
   uint32_t rcap_hint = 0;  // run-queue slots per key: grown when a batch's queues overflowed
+  // work history for the heavy-first job order: emitted event ids per key of each member query
+  // in the last batch (empty before the first), and the query map of the order (NfaArgs.qmap)
+  std::vector<double> qwork;
+  std::vector<uint32_t> qmap_h;
+  DBuf qmap;
   cep_batch_stats stats{};  // the last batch
   ~GroupRt() {
     if (mod) (void)hipModuleUnload(mod);
@@ -392,6 +397,26 @@ hipError_t launch_fn(hipFunction_t fn, NfaArgs& a, uint64_t blocks, hipStream_t 
 constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;   // output chunk ids are u32
 constexpr uint64_t kNodeMax = 0x7FFFFFF0ull;   // node / pointer ids: 31 bits (kPred0 tags a node's slot)
 
+// The heavy queries of a group from its work history `w` (emitted ids per key of each member
+// in the last batch): those within 16x of the heaviest, when the heaviest is > 4x the median
+// and they are at most half the group.  qmap = the heavy ones, then the others (index order).
+static uint32_t heavy_queries(const std::vector<double>& w, std::vector<uint32_t>& qmap) {
+  const size_t Q = w.size();
+  if (Q < 2) return 0;
+  std::vector<double> srt(w);
+  std::sort(srt.begin(), srt.end());
+  const double mx = srt.back(), med = srt[Q / 2];
+  if (!(mx > 0) || mx <= 4 * med) return 0;
+  qmap.clear();
+  for (size_t q = 0; q < Q; q++)
+    if (w[q] * 16 >= mx) qmap.push_back((uint32_t)q);
+  const uint32_t nh = (uint32_t)qmap.size();
+  if (nh == 0 || nh > Q / 2) return 0;
+  for (size_t q = 0; q < Q; q++)
+    if (w[q] * 16 < mx) qmap.push_back((uint32_t)q);
+  return nh;
+}
+
 // Runs a kernel group over the batch: the begin-hit bitmap and lane order, the matching
 // launch, re-runs of the jobs that hit a capacity limit or a deferred-walk conflict, and the
 // per-query compaction of the output chains into flat arrays.
@@ -552,6 +577,17 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
     if (const char* e = std::getenv("CEP_JOB_MAP")) a.job_map = (uint32_t)std::atoi(e);  // (measurement runs)
+    // Heavy-first: when the last batch's output was concentrated in a few queries (config 5:
+    // the 8 variants with the loosest dip predicate emit ~95 % of the event ids, their walks
+    // ~1000x longer than the others'), their jobs go first, so no heavy job is claimed late by
+    // a lane that then runs alone at the end of the launch.  Results do not depend on the order.
+    const uint32_t nh = heavy_queries(g.qwork, g.qmap_h);
+    if (nh > 0 && !std::getenv("CEP_NO_HEAVY_FIRST")) {
+      g.qmap.ensure(4 * Q);
+      HIPCHECK(hipMemcpyAsync(g.qmap.p, g.qmap_h.data(), 4 * Q, hipMemcpyHostToDevice, s->stream));
+      a.qmap = g.qmap.as<uint32_t>();
+      a.n_heavy = nh;
+    }
   }
   if (streaming) {  // walks deferred too: a conflict resolves exactly without a re-run (nfa_lane.h)
     a.rings = S.rings.p;
@@ -648,6 +684,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // re-run too).
   // The job lists are collected on the device; only their lengths come back.
   g.stats = cep_batch_stats{};
+  g.stats.heavy_first = a.qmap ? a.n_heavy : 0;
   g.stats.group_queries = (uint32_t)Q;
   float main_ms = 0;
   HIPCHECK(hipEventElapsedTime(&main_ms, s->ev2, s->ev1));
@@ -746,6 +783,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
     HIPCHECK(hipStreamSynchronize(s->stream));
     r.n_matches = tot[0];
     r.n_pairs = tot[1];
+    if (g.qwork.size() != Q) g.qwork.assign(Q, 0.0);
+    g.qwork[qi] = nk ? (double)(tot[0] + tot[1]) / (double)nk : 0.0;
     r.m_key.ensure(sizeof(uint32_t) * (tot[0] + 1));
     r.m_emit.ensure(sizeof(uint32_t) * (tot[0] + 1));
     r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));

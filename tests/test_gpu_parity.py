@@ -191,12 +191,19 @@ def test_cfg5_medium_bit_exact():
     qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)]
     s = N.Session(qs)
     s.push(off, cols)
-    total = 0
+    assert s.stats(0)["heavy_first"] == 0  # (no work history yet)
+    total, want = 0, []
     for i, q in enumerate(qs):
         r = oracle.run(q.ir, off, cols, threads=16)
         total += r["n_matches"]
+        want.append(r)
         assert_parity(session_result(s, i, off), r, off)
     assert total > 50000
+    # the second batch runs the heavy-first job order (the 8 dip-95 variants emit most ids)
+    s.push(off, cols)
+    assert s.stats(0)["heavy_first"] > 0
+    for i, r in enumerate(want):
+        assert_parity(session_result(s, i, off), r, off)
 
 
 @pytest.mark.parametrize("tier", TIERS)

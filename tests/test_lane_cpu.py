@@ -179,6 +179,18 @@ def test_lane_query_group():
         lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
 
 
+def test_lane_query_group_heavy_first(monkeypatch):
+    """The heavy-first job order of a group launch (NfaArgs.qmap: the heavy queries' jobs over
+    every key first, then the others'), with a heavy part whose size does not divide 64."""
+    monkeypatch.setenv("CEP_LANE_QMAP", "3")
+    cfg = W.SynthConfig("t", "stock", 70, 300, 0xCE90000 + 6)
+    off, cols = W.generate(cfg)
+    irs = [p.to_ir() for p in W.multi_queries(64)[48:64]]
+    res = lane_cpu.run_group(irs, off, cols)
+    for ir, g in zip(irs, res):
+        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+
+
 def test_dewey_short_compat_matches_general():
     """dewey.h dw_compat2 (the buffer walks' 2-pair fast path) equals dw_compatible on every
     pair of canonical versions of at most 2 RLE pairs over small digits."""
