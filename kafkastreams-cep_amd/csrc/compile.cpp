@@ -538,7 +538,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
   // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS"})
+  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:

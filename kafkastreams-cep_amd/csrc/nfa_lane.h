@@ -111,6 +111,10 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_QUIET_CHUNK
 #define CEP_QUIET_CHUNK 16
 #endif
+// partial drains (flush(may_stop)): 1 on, 0 off, 2 every flush stops as soon as it may (tests)
+#ifndef CEP_PARTIAL_DRAIN
+#define CEP_PARTIAL_DRAIN 1
+#endif
 #ifndef CEP_WALK_FLUSH
 #define CEP_WALK_FLUSH 24
 #endif
@@ -241,6 +245,7 @@ struct Lane {
   uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
   // deferred walks
   uint32_t wq_n = 0;  // queued
+  uint32_t wq_h = 0;  // queue slot of the oldest (the queue is a ring of wcap slots)
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
   uint32_t pl_n = 0;  // put-log entries since the last flush
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
@@ -265,6 +270,11 @@ struct Lane {
   }
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
+  }
+  // the slot of the i-th queued walk
+  __device__ __forceinline__ uint32_t wq_slot(uint32_t i) const {
+    const uint32_t q = wq_h + i;
+    return q >= A.wcap ? q - A.wcap : q;
   }
   __device__ __forceinline__ v4u* PL(uint32_t i) const { return wb + ((uint64_t)A.wcap * kWalkQuads + i) * 64; }
   // put-log entries one event may add at most (its records' puts): the wave drains before
@@ -695,14 +705,15 @@ struct Lane {
       return;
     }
     const Dewey v = dw_pin(v0);
-    *WQ(wq_n, 0) = v4u{sk | (flags << 8) | (v.n << 24), ev, first, v.len};
+    const uint32_t q = wq_slot(wq_n);
+    *WQ(q, 0) = v4u{sk | (flags << 8) | (v.n << 24), ev, first, v.len};
 #pragma unroll
     for (int k = 0; k < (kDeweyPairs + 1) / 2; k++)
       if ((uint32_t)(2 * k) < v.n)
-        *WQ(wq_n, 1 + k) = v4u{(uint32_t)v.v[2 * k], v.c[2 * k],
-                               2 * k + 1 < kDeweyPairs ? (uint32_t)v.v[2 * k + 1] : 0u,
-                               2 * k + 1 < kDeweyPairs ? v.c[2 * k + 1] : 0u};
-    reinterpret_cast<uint32_t*>(WQ(wq_n, kWalkQuads - 1))[0] = j;
+        *WQ(q, 1 + k) = v4u{(uint32_t)v.v[2 * k], v.c[2 * k],
+                            2 * k + 1 < kDeweyPairs ? (uint32_t)v.v[2 * k + 1] : 0u,
+                            2 * k + 1 < kDeweyPairs ? v.c[2 * k + 1] : 0u};
+    reinterpret_cast<uint32_t*>(WQ(q, kWalkQuads - 1))[0] = j;
     wq_n++;
     opc++;
   }
@@ -910,7 +921,12 @@ struct Lane {
 
   // Drains this lane's queue in order.  Called by every lane of the wave at once: the loop
   // gives each lane one node per iteration, starting its next walk as soon as one ends.
-  __device__ __forceinline__ void flush() {
+  // `may_stop` (partial drain): once at most half the lanes that had walks are still walking,
+  // this lane starts no further walk while fewer than kWalkFlush remain queued - the rest stay
+  // queued, in order, for a later flush (the wave goes back to its events instead of waiting
+  // for the longest queue).  Exact as any deferral: the put stamps and the put log cover the
+  // walks still queued (the log keeps the entries they can conflict with).
+  __device__ __forceinline__ void flush(bool may_stop = false) {
     CEP_STAT(5);
     if (wq_n) {  // this lane's walks may delete its nodes (no other lane's can)
       if (kCC > 0) cache_invalidate();
@@ -924,18 +940,30 @@ struct Lane {
     bool active = false;
     uint32_t cut = CEP_NONE;   // put-log entry of the first put a walk's delete makes throw
     uint32_t conf = CEP_NONE;  // the node of this step's conflicting delete
+#if CEP_PARTIAL_DRAIN == 1
+    const uint32_t n_start = (uint32_t)__popcll(__ballot(wq_n > 0));
+#endif
     for (;;) {
+#if CEP_PARTIAL_DRAIN == 1
+      const bool stop = may_stop && 2 * (uint32_t)__popcll(__ballot(true)) <= n_start;
+#elif CEP_PARTIAL_DRAIN == 2
+      const bool stop = may_stop;
+#else
+      const bool stop = false;
+#endif
       if (!active) {
         // (walks queued after the first put a conflict makes throw never run)
         if (i >= wq_n || err || (cut != CEP_NONE && id0 + i >= PL(cut)->y)) break;
-        const v4u h = *WQ(i, 0);
+        if (stop && wq_n - i < kWalkFlush) break;
+        const uint32_t qs = wq_slot(i);
+        const v4u h = *WQ(qs, 0);
         flags = (h.x >> 8) & 0xFF;
         w.n = h.x >> 24;
         w.len = h.w;
 #pragma unroll
         for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
           v4u d = {0, 0, 0, 0};
-          if ((uint32_t)(2 * k) < w.n) d = *WQ(i, 1 + k);
+          if ((uint32_t)(2 * k) < w.n) d = *WQ(qs, 1 + k);
           w.v[2 * k] = (int32_t)d.x;
           w.c[2 * k] = d.y;
           if (2 * k + 1 < kDeweyPairs) {
@@ -944,7 +972,7 @@ struct Lane {
           }
         }
         w = dw_pin(w);
-        t = reinterpret_cast<const uint32_t*>(WQ(i, kWalkQuads - 1))[0];
+        t = reinterpret_cast<const uint32_t*>(WQ(qs, kWalkQuads - 1))[0];
         i++;
         if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
         active = true;
@@ -976,8 +1004,24 @@ struct Lane {
       err = KE_ILLEGAL_STATE;
       err_seq = ce;
     }
+    if (i < wq_n && !err) {  // a partial drain: walks [i, wq_n) stay queued
+      wq_h = wq_slot(i);
+      wq_n -= i;
+      // the put-log entries a remaining walk (id >= id0 + i) can conflict with: put id > walk id
+      uint32_t k = 0;
+      for (uint32_t e = 0; e < pl_n; e++) {
+        const v4u x = *PL(e);
+        if (x.y > id0 + i) {
+          if (k != e) *PL(k) = x;
+          k++;
+        }
+      }
+      pl_n = k;
+      return;
+    }
     pl_n = 0;
     wq_n = 0;
+    wq_h = 0;
   }
 
   // ---------------------------------------------------------------- one event
@@ -1165,7 +1209,7 @@ struct Lane {
       CEP_PACC(8, 1);
       CEP_PT(tf0);
       if (A.defer && __any(wq_n >= kWalkFlush || pl_n + plog_margin() > kPutLog)) {
-        flush();
+        flush(pl_n + plog_margin() <= kPutLog);
         if (err) break;
       }
       CEP_PT(tf1);
@@ -1212,6 +1256,7 @@ struct Lane {
     n_matches = n_pairs = 0;
     out_first = CEP_NONE;
     wq_n = 0;
+    wq_h = 0;
     opc = 0;
     pl_n = 0;
     if (kCC > 0) {
@@ -1326,7 +1371,9 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
     CEP_PT(tf0);
     if (A.defer && (__any(has && (L.wq_n >= kWalkFlush || L.pl_n + L.plog_margin() > kPutLog)) ||
                     (ending && (__popcll(ending) >= kJobDrain || !__any(has && phase == 0))))) {
-      L.flush();  // every lane of the wave together (lanes without a queue leave at once)
+      // every lane of the wave together (lanes without a queue leave at once); lanes at their
+      // job's end drain all of theirs
+      L.flush(has && phase == 0 && L.pl_n + L.plog_margin() <= kPutLog);
       if (has && phase == 0 && L.err) phase = 2;  // a walk threw mid-job: the job stops there
       if (has && phase == 1) {
         L.finish_err();

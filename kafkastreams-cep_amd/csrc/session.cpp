@@ -641,7 +641,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.prof = s->prof.as<unsigned long long>();
   }
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
-  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming));
+  // ($CEP_STREAM_NARROW: a stream on the narrow build - no put log, so a walk conflict is a sticky
+  // error - and $CEP_STREAM_NO_ORDER: without the lane order; measurement runs only)
+  static const bool stream_narrow = std::getenv("CEP_STREAM_NARROW") != nullptr;
+  if (streaming && std::getenv("CEP_STREAM_NO_ORDER")) a.order = nullptr;
+  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
   Scratch h{};

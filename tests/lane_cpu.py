@@ -33,6 +33,8 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False):
     src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\w+\)\)\)", "", source or N.Query(ir).jit_source)
     if not narrow:
         src = "#define CEP_DEWEY_PAIRS 6\n" + src
+    # $CEP_LANE_DEFINES="A=1 B=2": tuning knobs of nfa_lane.h for this build (tests of the knobs)
+    src = "".join(f"#define {d.replace('=', ' ', 1)}\n" for d in os.environ.get("CEP_LANE_DEFINES", "").split()) + src
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
                    ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()

@@ -191,6 +191,43 @@ def test_lane_query_group_heavy_first(monkeypatch):
         lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
 
 
+@pytest.mark.parametrize("seed", list(range(0, 160, 16)) + [21, 80, 393, 571])
+def test_lane_partial_drains(seed, monkeypatch):
+    """Partial drains (nfa_lane.h flush(may_stop)) forced at every flush, with a 4-walk flush
+    threshold: walks stay queued across flushes and events, in order, and the put log keeps
+    the entries they can still conflict with (seeds 21-571: exact conflicts) - fuzz queries
+    per batch and as a stream."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_PARTIAL_DRAIN=2 CEP_WALK_FLUSH=4")
+    q = random_query(seed)
+    ir = q.to_ir()
+    if oracle.compile_check(ir):
+        pytest.skip("reference compile-time exception")
+    off, cols = random_stream(seed, 60, 14)
+    r = oracle.run(ir, off, cols)
+    g = lane_cpu.run(ir, off, cols)
+    lane_cpu.assert_same(g, r, off)
+    if seed in (21, 80, 393, 571):  # resolved through the log, no re-run
+        assert g["stats"]["exact_conflicts"] > 0 and g["retried"] == 0
+    batches = SS.split(off, cols, 3, seed=seed)
+    outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
+def test_lane_partial_drains_group(monkeypatch):
+    """The same on a kernel group (persistent lanes, config 5's heaviest variants) and the
+    config-4 stress query."""
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_PARTIAL_DRAIN=2 CEP_WALK_FLUSH=4")
+    cfg = W.SynthConfig("t", "stock", 40, 400, 0xCE90000 + 7)
+    off, cols = W.generate(cfg)
+    irs = [p.to_ir() for p in W.multi_queries(64)[52:64]]
+    for ir, g in zip(irs, lane_cpu.run_group(irs, off, cols)):
+        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+    ir = W.any_kleene_query(carry_volume=True).to_ir()
+    lane_cpu.assert_same(lane_cpu.run(ir, off, cols), oracle.run(ir, off, cols), off)
+
+
 def test_dewey_short_compat_matches_general():
     """dewey.h dw_compat2 (the buffer walks' 2-pair fast path) equals dw_compatible on every
     pair of canonical versions of at most 2 RLE pairs over small digits."""
