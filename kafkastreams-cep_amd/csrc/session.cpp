@@ -577,12 +577,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
     if (const char* e = std::getenv("CEP_JOB_MAP")) a.job_map = (uint32_t)std::atoi(e);  // (measurement runs)
-    // Heavy-first: when the last batch's output was concentrated in a few queries (config 5:
-    // the 8 variants with the loosest dip predicate emit ~95 % of the event ids, their walks
-    // ~1000x longer than the others'), their jobs go first, so no heavy job is claimed late by
-    // a lane that then runs alone at the end of the launch.  Results do not depend on the order.
+    // Heavy-first ($CEP_HEAVY_FIRST, opt-in): when the last batch's output was concentrated in
+    // a few queries (config 5: the 8 variants with the loosest dip predicate emit ~95 % of the
+    // event ids), their jobs go first.  Measured slower on config 5 (4.55 / 3.94 s against
+    // 3.81 / 2.95 s per batch, profiles/r03_cfg5_ab.sh): waves of heavy jobs only drain worse
+    // than the key-major waves, whose light lanes keep claiming jobs beside the heavy ones.
+    // Results do not depend on the order.
     const uint32_t nh = heavy_queries(g.qwork, g.qmap_h);
-    if (nh > 0 && !std::getenv("CEP_NO_HEAVY_FIRST")) {
+    if (nh > 0 && std::getenv("CEP_HEAVY_FIRST")) {
       g.qmap.ensure(4 * Q);
       HIPCHECK(hipMemcpyAsync(g.qmap.p, g.qmap_h.data(), 4 * Q, hipMemcpyHostToDevice, s->stream));
       a.qmap = g.qmap.as<uint32_t>();

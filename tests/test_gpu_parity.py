@@ -3,6 +3,8 @@
 Bit-exact on every array: match keys, emission events, walk pairs (stage, event) in
 reference order, per-key exception class and position, and the device checksum.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -199,9 +201,17 @@ def test_cfg5_medium_bit_exact():
         want.append(r)
         assert_parity(session_result(s, i, off), r, off)
     assert total > 50000
-    # the second batch runs the heavy-first job order (the 8 dip-95 variants emit most ids)
-    s.push(off, cols)
+    # the second batch with the heavy-first job order (opt-in: the 8 dip-95 variants' jobs first)
+    os.environ["CEP_HEAVY_FIRST"] = "1"
+    try:
+        s.push(off, cols)
+    finally:
+        del os.environ["CEP_HEAVY_FIRST"]
     assert s.stats(0)["heavy_first"] > 0
+    for i, r in enumerate(want):
+        assert_parity(session_result(s, i, off), r, off)
+    s.push(off, cols)  # (the default order again)
+    assert s.stats(0)["heavy_first"] == 0
     for i, r in enumerate(want):
         assert_parity(session_result(s, i, off), r, off)
 
