@@ -51,13 +51,38 @@ struct GroupPlan {
 };
 std::vector<GroupPlan> plan_groups(const std::vector<const cep_query*>& qs);
 
+// Measurement knobs ($CEP_* environment variables).  Read once, when a session
+// is created (tuning.cpp) - never on the launch path - and kept in the session.  Results never
+// depend on them; only the launch geometry and the time a batch takes do.
+struct Tuning {
+  uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
+  bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too
+  int spread = 2;               // $CEP_SPREAD: 0 off, 1 rows in order, 2 odd lanes reversed
+  uint32_t node_chunk = 0;      // $CEP_NODE_CHUNK: pool range per lane (0: default)
+  uint32_t out_chunk = 0;       // $CEP_OUT_CHUNK
+  uint32_t walk_cap = 0;        // $CEP_WALK_CAP: deferred walks per lane (0: default)
+  uint32_t walk_flush = 24;     // $CEP_WALK_FLUSH: the kernels' drain threshold (compile.cpp
+                                // compiles the same value in)
+  uint32_t job_map = 0;         // $CEP_JOB_MAP (nfa_lane.h job_id)
+  bool heavy_first = false;     // $CEP_HEAVY_FIRST: the heavy-first job order of groups
+  bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
+  bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
+  bool stream_no_order = false; // $CEP_STREAM_NO_ORDER
+  bool no_wm_fold = false;      // $CEP_NO_WM_FOLD: the watermark as its own pass
+  int stencil_pf = 0;           // $CEP_STENCIL_PF: 1, 2 or 4 (0: default)
+  bool host_trace = false;      // $CEP_HOST_TRACE: allocations and push phases on stderr
+};
+Tuning tuning_from_env();
+// the drain threshold the JIT kernels are compiled with ($CEP_WALK_FLUSH, default 24)
+uint32_t tuning_walk_flush();
+
 struct NfaArgs;
 struct StencilArgs;
 struct KeyState;
 
 hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_len, hipStream_t st);
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap);  // double-buffered run queues
-uint64_t walkq_size(uint64_t n_slots, uint32_t wcap);        // deferred-walk queues
+uint64_t walkq_size(uint64_t n_slots, uint32_t wcap, uint32_t plog);  // deferred-walk queues + put logs
 hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list, uint32_t* conf_list,
                                 uint32_t* counts, hipStream_t st);
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
@@ -77,7 +102,7 @@ hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, cons
 hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
                             uint32_t* zero, uint32_t n_zero, hipStream_t st);
 uint64_t stencil_waves(uint64_t n_events);
-hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
+hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, int pf, hipStream_t st);
 uint64_t stencil_tiles(uint64_t n_events);
 hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
                                     void* price, void* volume, int32_t* status, uint32_t* name_span,

@@ -168,4 +168,12 @@ enum Bc : uint8_t {
   BC_JT,       // arg = target word: top true -> jump keeping it, else pop
 };
 
+// put-log entries per lane of the deferred-walk queues (nfa_lane.h): every put one event can
+// log (2 * rcap + 4 for rcap records) fits twice over, at least kPutLogMin
+constexpr uint32_t kPutLogMin = 256;
+__host__ __device__ inline uint32_t put_log_entries(uint32_t rcap) {
+  const uint64_t need = 2ull * (2ull * rcap + 4);
+  return need > kPutLogMin ? (uint32_t)need : kPutLogMin;
+}
+
 }  // namespace cep

@@ -4,6 +4,7 @@
 // Matcher / Aggregator (pattern/Matcher.java, pattern/Aggregator.java), which arrive as the
 // typed IR documented in include/cep.h.  Host-only code, linked into libcep.so.
 #include <algorithm>
+#include <functional>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -538,7 +539,9 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
   // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
-  for (const char* knob : {"CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN"})
+  // (the drain threshold: session.cpp sizes streams' walk queues by the same tuning value)
+  if (tuning_walk_flush() != 24) o += "#define CEP_WALK_FLUSH " + std::to_string(tuning_walk_flush()) + "\n";
+  for (const char* knob : {"CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN", "CEP_EST_MODE"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:
@@ -661,7 +664,69 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   if (const char* v = std::getenv("CEP_RING_LDS")) rl = "(" + rl + " < " + std::to_string(std::atoi(v)) + " ? " + rl + " : " + std::to_string(std::atoi(v)) + ")";
   o += "  static constexpr uint32_t kRingLds = " + rl + ";\n";
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
+  // Wave-cooperative record steps (nfa_coop.h): the static bounds of one queued record's step -
+  // puts, records produced, walks (+ removePattern's) - over the stages a queued record can be
+  // at, and the stage keys it can put.  Needs the begin run in registers, no queued record
+  // putting the begin stage's key, distinct stage keys along every PROCEED chain (a record
+  // puts a stage key at most once per event), and bounds the capture holds; kernel groups
+  // keep the per-lane loop.
+  {
+    struct Bnd {
+      int p = 0, o = 0, w = 0;
+      uint32_t sks = 0;
+      bool ok = true;
+    };
+    std::function<Bnd(int)> bnd = [&](int si) -> Bnd {
+      const DevStage& S = d.st[si];
+      Bnd r;
+      if (S.type == ST_FINAL) return r;
+      bool hT = false, hB = false, hI = false;
+      int proc = -1;
+      for (int e = 0; e < S.n_edges; e++) {
+        if (S.e[e].op == OP_TAKE) hT = true;
+        if (S.e[e].op == OP_BEGIN) hB = true;
+        if (S.e[e].op == OP_IGNORE) hI = true;
+        if (S.e[e].op == OP_PROCEED) proc = (int)S.e[e].target;
+      }
+      Bnd t;
+      if (proc >= 0 && proc != si) t = bnd(proc);
+      if (proc == si) t.ok = false;  // (never built: a stage's PROCEED goes to its successor)
+      const bool hP = proc >= 0, cons = hT || hB;
+      const bool canBr = (hP && hT) || (hI && hT) || (hI && hB) || (hI && hP);
+      r.p = (cons ? 1 : 0) + t.p;
+      const int nb = std::max((cons || hI) ? 1 : 0, t.o);
+      const int br = canBr ? (hB ? 1 : 0) + t.o + 1 : 0;
+      r.o = std::max(nb, br);
+      r.w = (canBr ? 1 : 0) + t.w;
+      r.sks = (cons ? 1u << S.sk : 0u) | t.sks;
+      r.ok = t.ok && !(cons && ((t.sks >> S.sk) & 1u));
+      return r;
+    };
+    Bnd all;
+    all.w = 1;  // removePattern
+    for (uint32_t si = 0; si < d.n_stages; si++) {
+      if (si == d.begin_stage || d.st[si].type == ST_FINAL) continue;
+      const Bnd b = bnd((int)si);
+      all.p = std::max(all.p, b.p);
+      all.o = std::max(all.o, b.o);
+      all.w = std::max(all.w, b.w);
+      all.sks |= b.sks;
+      all.ok = all.ok && b.ok;
+    }
+    const bool coop = quiet && !lits.param && all.ok && !((all.sks >> bs.sk) & 1u) && all.p <= 4 && all.o <= 4 &&
+                      all.w <= 4;
+    o += "  static constexpr bool kCoop = " + std::string(coop ? "true" : "false") + ";  // nfa_coop.h\n";
+    o += "  static constexpr int kCoopP = " + std::to_string(std::max(all.p, 1)) + ", kCoopO = " +
+         std::to_string(std::max(all.o, 1)) + ", kCoopW = " + std::to_string(std::max(all.w, 1)) + ";\n";
+    o += "  static constexpr uint32_t kCoopSkMask = " + std::to_string(coop ? all.sks : 0u) + "u;\n";
+  }
   o += "  typedef Ev EvT;\n";
+  // another lane's event fields (coop pages step other lanes' records)
+  o += "  __device__ __forceinline__ Ev shfl_ev(const Ev& e, uint32_t src) const {\n    Ev r;\n";
+  for (uint32_t f = 0; f < d.n_fields; f++)
+    if (fields[f]) o += "    r.f" + std::to_string(f) + " = __shfl(e.f" + std::to_string(f) + ", src, 64);\n";
+  o += ts ? "    r.ts = __shfl(e.ts, src, 64);\n" : "    r.ts = 0;\n";
+  o += "    return r;\n  }\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
   o += "  __device__ __forceinline__ void set_query(uint32_t qi) { ld_kc(K, A, qi); }\n";
   o += "  __device__ __forceinline__ void load_ev(Ev& e, uint64_t pos) const { ld_ev(e, A, pos); }\n";
@@ -900,11 +965,16 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "    uint64_t bits = A.bhits[wi];\n    const uint64_t s = wi << 6;\n";
     o += "    if (s < base) bits &= ~0ull << (base - s);\n";
     o += "    if (p1 - s < 64) bits &= (1ull << (p1 - s)) - 1ull;\n";
+    // ($CEP_EST_MODE=1 at query compile, measurement runs: the span after the first begin hit,
+    // max instead of sum)
     o += "    while (bits) {\n      const uint32_t b = (uint32_t)__builtin_ctzll(bits);\n      bits &= bits - 1ull;\n";
-    o += "      w += n - (uint32_t)(s + b - base);\n    }\n  }\n";
+    o += "      const uint64_t r = n - (uint32_t)(s + b - base);\n";
+    o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n      w = w > r ? w : r;\n#else\n      w += r;\n#endif\n    }\n  }\n";
     // (ordering by the span after the first begin hit instead, or by span then mean live
     // runs, was measured: cfg 3 31.5 -> 34.1 / 33.2 ms)
-    o += "  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n";
+    o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n";
+    o += "  for (int o = 32; o > 0; o >>= 1) {\n    const uint64_t y = __shfl_down(w, o, 64);\n    w = y > w ? y : w;\n  }\n";
+    o += "#else\n  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n#endif\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n";

@@ -26,8 +26,10 @@ struct NfaArgs {
   const int64_t* ts;
   void* rings;               // Rec<F>[n_slots * rcap]
   uint32_t rcap;
-  void* walks;               // deferred-walk queues, wcap per slot (nfa_lane.h)
+  void* walks;               // deferred-walk queues, wcap per slot, then plog put-log entries (nfa_lane.h)
   uint32_t wcap;
+  uint32_t plog;             // put-log entries per slot: room for every put one event can log
+                             // (2 * rcap + 4) twice over, at least kPutLogMin (session.cpp)
   uint32_t defer;            // 1: queue buffer walks and drain them wave-wide; 0: walk in place
   // Jobs: a job is (query qi of the launch, key), id qi * n_keys + key.  Without a job list, job
   // index i is query i % n_q on the key of rank i / n_q, rank -> key through `order` (lane

@@ -42,6 +42,9 @@ struct InterpQ {
   static constexpr bool kBeginReg = false;  // quiet is only known at run time here
   static constexpr bool kFold32 = false;     // fold slots hold any state type
   static constexpr uint32_t kRingLds = 0;    // LDS holds the DevQuery and bytecode: queues in HBM
+  static constexpr bool kCoop = false;       // records stepped per lane (nfa_coop.h needs kBeginReg)
+  static constexpr int kCoopP = 1, kCoopO = 1, kCoopW = 1;
+  static constexpr uint32_t kCoopSkMask = 0;
   struct EvT {};                             // the programs read the columns themselves
 
   __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {
@@ -554,7 +557,7 @@ hipError_t launch_nfa(int F, const NfaArgs& a, uint64_t nslots, uint32_t code_le
   }
 }
 
-uint64_t walkq_size(uint64_t n_slots, uint32_t wcap) { return walkq_bytes(n_slots, wcap); }
+uint64_t walkq_size(uint64_t n_slots, uint32_t wcap, uint32_t plog) { return walkq_bytes(n_slots, wcap, plog); }
 
 uint64_t ring_size(int F, uint64_t n_slots, uint32_t rcap) {
   return ring_bytes(F <= 2 ? 2 : (F <= 4 ? 4 : 8), n_slots, rcap);

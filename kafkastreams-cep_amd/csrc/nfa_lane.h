@@ -140,8 +140,9 @@ constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
 constexpr uint32_t kWalkHint = 8;
 // put-log entries per lane ({node, walks queued, event, -}), after each 64 lanes' walk queues
 // in A.walks (the log's address is the walk queue's plus a launch constant); the wave drains
-// its walks before an event could overflow it
-constexpr uint32_t kPutLog = 256;
+// its walks before an event could overflow it.  A.plog entries per lane, sized by the host from
+// the run-queue capacity (put_log_entries): every put one event can log fits twice over.
+// (put_log_entries, cep_layout.h)
 // The narrow build of a query (compile.cpp) leaves the put log out - the registers it costs
 // spill there - and reports a conflict as KE_CONFLICT: the key is re-run in the wide build,
 // which resolves it.  (Default: on.)
@@ -172,6 +173,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4), may_alias));
 #define CEP_LDS_AS __attribute__((address_space(3)))
 #endif
 typedef CEP_LDS_AS v4u lds_v4u;
+}  // namespace cep
+#include "nfa_coop.h"
+namespace cep {
 
 // W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
 template <int F, bool W32 = false>
@@ -204,12 +208,14 @@ __host__ __device__ inline uint64_t ring_bytes(int F, uint64_t n_slots, uint32_t
   return ((n_slots + 63) / 64) * 64ull * 2ull * rcap * quads * 16ull;
 }
 
-// bytes of deferred-walk queues for n_slots lanes of wcap walks and their put logs
-__host__ __device__ inline uint64_t walkq_bytes(uint64_t n_slots, uint32_t wcap) {
-  return ((n_slots + 63) / 64) * 64ull * (wcap * kWalkQuads + kPutLog) * 16ull;
+// bytes of deferred-walk queues for n_slots lanes of wcap walks and their put logs (plog entries)
+__host__ __device__ inline uint64_t walkq_bytes(uint64_t n_slots, uint32_t wcap, uint32_t plog) {
+  return ((n_slots + 63) / 64) * 64ull * ((uint64_t)wcap * kWalkQuads + plog) * 16ull;
 }
 // quads per 64 lanes of that allocation
-__host__ __device__ inline uint64_t walkq_group_quads(uint32_t wcap) { return (wcap * (uint64_t)kWalkQuads + kPutLog) * 64; }
+__host__ __device__ inline uint64_t walkq_group_quads(uint32_t wcap, uint32_t plog) {
+  return ((uint64_t)wcap * kWalkQuads + plog) * 64;
+}
 
 template <int F, class Q>
 struct Lane {
@@ -236,6 +242,7 @@ struct Lane {
   uint32_t ochunk = CEP_NONE, opos = 0;
   uint32_t ocur = 0, oend = 0;  // output chunks in hand (kept across the jobs of a persistent lane)
   uint32_t cur_first = CEP_NONE;  // node chain of event j
+  uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending; coop pages)
   // chain cache (kCC > 0): packed stage keys (byte k) | count << 24 (> kCC: overflow/invalid)
   uint32_t cc_pack = (kCC + 1u) << 24, pc_pack = (kCC + 1u) << 24;
   uint32_t cc_id[kCCs], pc_id[kCCs];
@@ -265,8 +272,8 @@ struct Lane {
 
   __device__ Lane(const NfaArgs& a, Q& qq) : A(a), q(qq) {}
 
-  __device__ __forceinline__ v4u* QP(uint32_t h, uint32_t slot, int quad) const {
-    return rb + ((uint64_t)(h * A.rcap + slot) * Lay::kQuads + quad) * 64;
+  __device__ __forceinline__ v4u* QP(uint32_t h, uint32_t slot, int quad, v4u* b = nullptr) const {
+    return (b ? b : rb) + ((uint64_t)(h * A.rcap + slot) * Lay::kQuads + quad) * 64;
   }
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
@@ -279,7 +286,7 @@ struct Lane {
   __device__ __forceinline__ v4u* PL(uint32_t i) const { return wb + ((uint64_t)A.wcap * kWalkQuads + i) * 64; }
   // put-log entries one event may add at most (its records' puts): the wave drains before
   __device__ __forceinline__ uint32_t plog_margin() const {
-    return 2 * A.rcap + 4 < kPutLog / 2 ? 2 * A.rcap + 4 : kPutLog / 2;
+    return 2 * A.rcap + 4 < A.plog / 2 ? 2 * A.rcap + 4 : A.plog / 2;
   }
   __device__ __forceinline__ lds_v4u* LQ(uint32_t h, uint32_t slot, int lq) const {
     return lr + ((h * kRL + slot) * Lay::kLdsQuads + lq) * 64;
@@ -288,13 +295,17 @@ struct Lane {
   __device__ __forceinline__ bool lds_slot(uint32_t slot, int quad) const {
     return kRL > 0 && Lay::in_lds(quad) && slot < kRL;
   }
-  __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad) const {
-    if (lds_slot(slot, quad)) return *LQ(h, slot, Lay::lds_quad(quad));
-    return *QP(h, slot, quad);
+  // Another lane's queue (nfa_coop.h steps other keys' records): `d` lanes from this one for
+  // the LDS slots (the lanes of a block are interleaved at 16 B), `b` its HBM base (a stream's
+  // queue lives at its key's position, not its lane's)
+  __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad, int d = 0, v4u* b = nullptr) const {
+    if (lds_slot(slot, quad)) return *(LQ(h, slot, Lay::lds_quad(quad)) + d);
+    return *QP(h, slot, quad, b);
   }
-  __device__ __forceinline__ void wr(uint32_t h, uint32_t slot, int quad, const v4u& v) const {
-    if (lds_slot(slot, quad)) *LQ(h, slot, Lay::lds_quad(quad)) = v;
-    else *QP(h, slot, quad) = v;
+  __device__ __forceinline__ void wr(uint32_t h, uint32_t slot, int quad, const v4u& v, int d = 0,
+                                     v4u* b = nullptr) const {
+    if (lds_slot(slot, quad)) *(LQ(h, slot, Lay::lds_quad(quad)) + d) = v;
+    else *QP(h, slot, quad, b) = v;
   }
   // streaming: the LDS slots of the queue (half `half`, `count` records) <-> their HBM positions
   __device__ __forceinline__ void lds_spill(bool to_hbm) {
@@ -310,8 +321,9 @@ struct Lane {
 
   // ---------------------------------------------------------------- records
   // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
-  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf) const {
-    const v4u hd = rd(h, slot, 0);
+  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf, int d = 0,
+                                       v4u* b = nullptr) const {
+    const v4u hd = rd(h, slot, 0, d, b);
     r.stage = hd.x & 0x00FFFFFFu;
     r.event = hd.y;
     r.ev_first = hd.z == kPending ? pf : hd.z;
@@ -319,13 +331,13 @@ struct Lane {
     r.ver.n = hd.x >> 24;
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++) {
-      v4u d = {0, 0, 0, 0};
-      if ((uint32_t)(2 * k) < r.ver.n) d = rd(h, slot, 1 + k);
-      r.ver.v[2 * k] = (int32_t)d.x;
-      r.ver.c[2 * k] = d.y;
+      v4u dq = {0, 0, 0, 0};
+      if ((uint32_t)(2 * k) < r.ver.n) dq = rd(h, slot, 1 + k, d, b);
+      r.ver.v[2 * k] = (int32_t)dq.x;
+      r.ver.c[2 * k] = dq.y;
       if (2 * k + 1 < kDeweyPairs) {
-        r.ver.v[2 * k + 1] = (int32_t)d.z;
-        r.ver.c[2 * k + 1] = d.w;
+        r.ver.v[2 * k + 1] = (int32_t)dq.z;
+        r.ver.c[2 * k + 1] = dq.w;
       }
     }
     uint32_t len = 0;  // DeweyVersion.length(): the digits of every pair
@@ -336,11 +348,11 @@ struct Lane {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++) {
-      const v4u d = rd(h, slot, 1 + Lay::kDwQuads + k);
-      w[4 * k] = d.x;
-      w[4 * k + 1] = d.y;
-      w[4 * k + 2] = d.z;
-      w[4 * k + 3] = d.w;
+      const v4u fq = rd(h, slot, 1 + Lay::kDwQuads + k, d, b);
+      w[4 * k] = fq.x;
+      w[4 * k + 1] = fq.y;
+      w[4 * k + 2] = fq.z;
+      w[4 * k + 3] = fq.w;
     }
     r.nullmask = w[0];
 #pragma unroll
@@ -349,18 +361,20 @@ struct Lane {
   }
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
-                                             uint32_t ev_first, const Dewey& ver0, uint32_t node) {
+                                             uint32_t ev_first, const Dewey& ver0, uint32_t node, int d = 0,
+                                             v4u* b = nullptr) {
     const Dewey ver = dw_pin(ver0);
-    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, node});
+    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, node}, d, b);
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
         wr(h, slot, 1 + k, v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
                                2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
-                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u});
+                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u}, d, b);
   }
 
-  __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm) {
+  __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm, int d = 0,
+                                              v4u* b = nullptr) {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int i = 0; i < Lay::kFoldQuads * 4; i++) w[i] = 0;
@@ -376,7 +390,7 @@ struct Lane {
     }
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++)
-      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]});
+      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]}, d, b);
   }
 
   __device__ __forceinline__ void copy_rec(uint32_t h, uint32_t from, uint32_t to) {
@@ -458,9 +472,9 @@ struct Lane {
     return CEP_NONE;
   }
 
-  __device__ __forceinline__ void write_pred(uint32_t p, uint32_t prev, const Dewey& v0) {
+  __device__ __forceinline__ void write_pred(uint32_t p, uint32_t prev, const Dewey& v0, uint32_t next = CEP_NONE) {
     const Dewey v = dw_pin(v0);
-    *PQ(p, 0) = v4u{prev, CEP_NONE, v.n << 8, v.len};
+    *PQ(p, 0) = v4u{prev, next, v.n << 8, v.len};
 #pragma unroll
     for (int k = 0; k < (kDeweyPairs + 1) / 2; k++)
       if ((uint32_t)(2 * k) < v.n)
@@ -547,7 +561,7 @@ struct Lane {
     }
 #if CEP_PUT_LOG
     if (A.defer && wq_n > 0) {  // found live while walks are queued: stamp and log (conflict check)
-      if (pl_n >= kPutLog) {        // (only an event with more puts than plog_margin())
+      if (pl_n >= A.plog) {         // (only an event with more puts than plog_margin())
         err = A.carry ? KE_CAPACITY : KE_CONFLICT;
         return CEP_NONE;
       }
@@ -919,16 +933,18 @@ struct Lane {
     if (!err) walk_end(flags, npa, np);
   }
 
-  // Drains this lane's queue in order.  Called by every lane of the wave at once: the loop
-  // gives each lane one node per iteration, starting its next walk as soon as one ends.
+  // Drains this lane's queue in order.  Called by every lane of the wave at once (convergent:
+  // the loop's cross-lane operations see every lane; `part` false: this lane takes part with
+  // nothing to walk): the loop gives each lane one node per iteration, starting its next walk
+  // as soon as one ends.
   // `may_stop` (partial drain): once at most half the lanes that had walks are still walking,
   // this lane starts no further walk while fewer than kWalkFlush remain queued - the rest stay
   // queued, in order, for a later flush (the wave goes back to its events instead of waiting
   // for the longest queue).  Exact as any deferral: the put stamps and the put log cover the
   // walks still queued (the log keeps the entries they can conflict with).
-  __device__ __forceinline__ void flush(bool may_stop = false) {
+  __device__ __forceinline__ void flush(bool may_stop = false, bool part = true) {
     CEP_STAT(5);
-    if (wq_n) {  // this lane's walks may delete its nodes (no other lane's can)
+    if (part && wq_n) {  // this lane's walks may delete its nodes (no other lane's can)
       if (kCC > 0) cache_invalidate();
       clear_hints();
     }
@@ -937,24 +953,35 @@ struct Lane {
     uint64_t npa = 0;
     Dewey w;
     dw_init(w, 0);
-    bool active = false;
+    bool active = false, draining = part;
     uint32_t cut = CEP_NONE;   // put-log entry of the first put a walk's delete makes throw
     uint32_t conf = CEP_NONE;  // the node of this step's conflicting delete
 #if CEP_PARTIAL_DRAIN == 1
-    const uint32_t n_start = (uint32_t)__popcll(__ballot(wq_n > 0));
+    const uint32_t n_start = (uint32_t)__popcll(__ballot(part && wq_n > 0));
 #endif
     for (;;) {
+      const uint64_t in = __ballot(draining);  // the lanes still draining
+      if (!in) break;
 #if CEP_PARTIAL_DRAIN == 1
-      const bool stop = may_stop && 2 * (uint32_t)__popcll(__ballot(true)) <= n_start;
+      const bool stop = may_stop && 2 * (uint32_t)__popcll(in) <= n_start;
 #elif CEP_PARTIAL_DRAIN == 2
       const bool stop = may_stop;
 #else
       const bool stop = false;
 #endif
+      if (!draining) continue;
       if (!active) {
         // (walks queued after the first put a conflict makes throw never run)
-        if (i >= wq_n || err || (cut != CEP_NONE && id0 + i >= PL(cut)->y)) break;
-        if (stop && wq_n - i < kWalkFlush) break;
+        if (i >= wq_n || err || (cut != CEP_NONE && id0 + i >= PL(cut)->y)) {
+          draining = false;
+          continue;
+        }
+        // (no partial stop once a conflict was found: every walk queued before that put runs
+        // first, as in the reference, before the key stops at the put's event)
+        if (stop && cut == CEP_NONE && wq_n - i < kWalkFlush) {
+          draining = false;
+          continue;
+        }
         const uint32_t qs = wq_slot(i);
         const v4u h = *WQ(qs, 0);
         flags = (h.x >> 8) & 0xFF;
@@ -974,7 +1001,10 @@ struct Lane {
         w = dw_pin(w);
         t = reinterpret_cast<const uint32_t*>(WQ(qs, kWalkQuads - 1))[0];
         i++;
-        if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) break;
+        if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) {
+          draining = false;
+          continue;
+        }
         active = true;
       }
       CEP_STAT(7);
@@ -984,17 +1014,22 @@ struct Lane {
         conf = CEP_NONE;
         if (k == CEP_NONE) {  // (a stamp without its log entry: never; re-run to be safe)
           walk_fail(A.carry ? KE_CAPACITY : KE_CONFLICT, t);
-          break;
+          draining = false;
+          continue;
         }
         CEP_STAT(8);
         if (cut == CEP_NONE || PL(k)->y < PL(cut)->y) cut = k;  // (the earliest such put)
       }
       if (!more) {
-        if (err) break;
+        if (err) {
+          draining = false;
+          continue;
+        }
         walk_end(flags, npa, np);
         active = false;
       }
     }
+    if (!part) return;
     if (cut != CEP_NONE && !err) {  // IllegalState at that put's event: its matches dropped
       const uint32_t ce = PL(cut)->z;
       if (wt_last == ce) {
@@ -1025,11 +1060,15 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- one event
-  __device__ __forceinline__ void event(bool begin_hit) {
+  // event() = event_pre(), the records (event_records() per lane, or coop_records() over the
+  // wave: nfa_coop.h), event_post(): the begin run, the queue swap and the finals.
+  EvT nev;             // the next event's fields, prefetched by event_pre (consumed at the next event)
+  bool nmore = false;  // there is a next event
+
+  __device__ __forceinline__ void event_pre() {
     CEP_STAT(0);
     CEP_PACC(10, 1);
-    CEP_PT(te0);
-    const uint32_t pf = cur_first;  // node chain of the previous event: resolves kPending
+    pf_ev = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
     if (kCC > 0) {  // the last event() call's nodes are the previous event's if it was j - 1
       pc_pack = ev_last + 1 == j ? cc_pack : (kCC + 1u) << 24;
@@ -1040,15 +1079,19 @@ struct Lane {
     }
     n_final = 0;
     ocount = 0;
-    // prefetch the next event's fields (consumed by the next event() call)
-    EvT nev = ev;
-    const bool more = j + 1 < j0 + n_ev;
-    if (more) q.load_ev(nev, base + j + 1);
+    // prefetch the next event's fields (consumed by the next event)
+    nev = ev;
+    nmore = j + 1 < j0 + n_ev;
+    if (nmore) q.load_ev(nev, base + j + 1);
+  }
+
+  // the queued records, one after another (NFA.java:99-107)
+  __device__ __forceinline__ void event_records() {
     const uint32_t n = count;
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
       CEP_STAT(1);
-      load(half, i, c, pf);
+      load(half, i, c, pf_ev);
       const int produced = q.step(*this, c);
       if (err) return;
       CEP_PACC(9, 1);
@@ -1057,8 +1100,10 @@ struct Lane {
         if (err) return;
       }
     }
+  }
+
+  __device__ __forceinline__ void event_post(bool begin_hit) {
     CEP_PT(te1);
-    CEP_PACC(2, te1 - te0);
     // the begin run, last in the queue: its predicate runs after every other record's
     // (an exception from it must not pre-empt theirs)
     if (kBeginReg && !begin_hit) {
@@ -1083,7 +1128,7 @@ struct Lane {
     const uint32_t oh = half ^ 1u;
     half = oh;
     count = ocount;
-    if (more) {
+    if (nmore) {
       ev = nev;
       ev_pos = j + 1;
     }
@@ -1111,6 +1156,254 @@ struct Lane {
     CEP_PACC(4, te4 - te2);
   }
 
+  __device__ __forceinline__ void event(bool begin_hit) {
+    CEP_PT(te0);
+    event_pre();
+    event_records();
+    CEP_PT(te9);
+    CEP_PACC(2, te9 - te0);
+    if (err) return;
+    event_post(begin_hit);
+  }
+
+  // ---------------------------------------------------------------- cooperative records
+  // The records of every lane's current event stepped as one flat list, 64 per page, the side
+  // effects resolved in record order (nfa_coop.h).  Convergent: every lane of the wave calls
+  // it; `act`: this lane's key has an event now (event_pre done).  On return each acting lane's
+  // key is as event_records() would have left it: its next queue half holds the records
+  // produced, its node chain and walk queue hold the puts and walks, err the first exception.
+  __device__ __forceinline__ void coop_records(bool act) {
+    using X_t = RecCtx<F, Q>;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n_own = act ? count : 0u;
+    const uint32_t incl0 = wave_incl_scan(n_own);
+    const uint32_t excl0 = incl0 - n_own;
+    const uint32_t total = __shfl(incl0, 63, 64);
+    // per stage key a record can put: this key's node of (sk, j) and its last pointer, as earlier
+    // pages left them (CEP_NONE: none yet)
+    uint32_t nodeJ[kMaxStageKeys], tailJ[kMaxStageKeys];
+#pragma unroll
+    for (uint32_t sk = 0; sk < (uint32_t)kMaxStageKeys; sk++) {
+      nodeJ[sk] = CEP_NONE;
+      tailJ[sk] = CEP_NONE;
+    }
+    for (uint32_t pb = 0; pb < total; pb += 64) {  // (wave-uniform)
+      const uint32_t r = pb + lane;
+      const bool valid = r < total;
+      // the owner: the last lane whose records start at or before r (it has records: r < total)
+      uint32_t o = 0;
+#pragma unroll
+      for (uint32_t b = 32; b > 0; b >>= 1) {
+        const uint32_t e = __shfl(excl0, o + b, 64);
+        if (e <= r) o += b;
+      }
+      const uint32_t ex_o = __shfl(excl0, o, 64), n_o = __shfl(n_own, o, 64);
+      const int d = (int)o - (int)lane;
+      v4u* const rb_o = reinterpret_cast<v4u*>(__shfl((unsigned long long)rb, o, 64));
+      // this record's key's lanes in the page, and this lane's own key's lanes (owner role)
+      const uint64_t wseg = valid ? lanes_range(ex_o > pb ? ex_o - pb : 0u, ex_o + n_o - pb < 64 ? ex_o + n_o - pb : 64u)
+                                  : 0ull;
+      const uint64_t oseg = (n_own && excl0 < pb + 64 && excl0 + n_own > pb)
+                                ? lanes_range(excl0 > pb ? excl0 - pb : 0u, excl0 + n_own - pb < 64 ? excl0 + n_own - pb : 64u)
+                                : 0ull;
+      const uint64_t below = lanes_below(lane) & wseg;
+      // the owner's context
+      const uint32_t h_o = __shfl(half, o, 64), j_o = __shfl(j, o, 64), pf_o = __shfl(pf_ev, o, 64);
+      const uint32_t key_o = __shfl(key, o, 64), err_o = __shfl((uint32_t)err, o, 64);
+      X_t X(A);
+      X.ev = q.shfl_ev(ev, o);
+      X.j = j_o;
+      X.base = base;
+      int produced = 0;
+      if (valid && !err_o) {
+        CEP_STAT(1);
+        Rec<F> c;
+        load(h_o, r - ex_o, c, pf_o, d, rb_o);
+        produced = q.step(X, c);
+        if (!X.err && produced == 0)  // removePattern
+          X.walk_remove(q.stage_sk(c.stage), c.event, c.ev_first, c.ver, false, (c.stage & kRecEps) ? c.node : CEP_NONE);
+      }
+      // ---- the first exception of each key: records after it take no effect; its own puts
+      // (their stamps) and walks made before it stand, its records do not
+      const bool stepped = valid && !err_o;
+      const uint64_t eb = __ballot(stepped && X.err != KE_OK);
+      const bool live = stepped && !(eb & below);
+      const bool full = live && X.err == KE_OK;  // records and nodes too
+      bool retry = false;     // a pool or the run queue ran out: the key is re-run (KE_RETRY)
+      bool conflict = false;  // the walk queue or the put log ran out: re-run with walks in place
+      // ---- walks: slots in the owner's queue, in record order
+      const uint32_t wq_n_o = __shfl(wq_n, o, 64), wq_h_o = __shfl(wq_h, o, 64), opc_o = __shfl(opc, o, 64);
+      const uint32_t nw = live ? X.nw : 0u;
+      const uint32_t wi = wave_incl_scan(nw);
+      const uint32_t wlo = low_lane(wseg, lane);
+      const uint32_t wb0 = __shfl(wi, wlo ? wlo - 1 : 0, 64);
+      const uint32_t wbefore = wi - nw - (wlo ? wb0 : 0u);  // walks of the key's earlier records in the page
+      // ---- put stamps (the conflict check, nfa_lane.h): a predecessor found live while walks
+      // are queued, stamped with the key's walk count before the record
+#if CEP_PUT_LOG
+      const uint32_t pl_n_o = __shfl(pl_n, o, 64);
+      uint32_t nst = 0;
+      if (live && A.defer && wq_n_o + wbefore > 0)
+#pragma unroll
+        for (int k = 0; k < X_t::kP; k++)
+          if ((uint32_t)k < X.np && X.p_prev[k] != CEP_NONE) nst++;
+      const uint32_t si = wave_incl_scan(nst);
+      const uint32_t sb0 = __shfl(si, wlo ? wlo - 1 : 0, 64);
+      uint32_t sslot = pl_n_o + si - nst - (wlo ? sb0 : 0u);
+#endif
+      if (live && A.defer && wq_n_o + wbefore > 0) {
+#pragma unroll
+        for (int k = 0; k < X_t::kP; k++)
+          if ((uint32_t)k < X.np && X.p_prev[k] != CEP_NONE) {
+            A.nodes[X.p_prev[k]].lk = opc_o + wbefore;
+#if CEP_PUT_LOG
+            if (sslot >= A.plog) conflict = true;
+            else *(PL(sslot) + d) = v4u{X.p_prev[k], opc_o + wbefore, j_o, 0u};
+            sslot++;
+#endif
+          }
+      }
+      // the walks themselves
+      if (nw) {
+#pragma unroll
+        for (int k = 0; k < X_t::kW; k++)
+          if ((uint32_t)k < nw) {
+            const uint32_t idx = wq_n_o + wbefore + (uint32_t)k;
+            if (idx >= A.wcap) {
+              conflict = true;
+            } else {
+              const uint32_t qs = wq_h_o + idx >= A.wcap ? wq_h_o + idx - A.wcap : wq_h_o + idx;
+              const Dewey v = dw_pin(X.w_ver[k]);
+              *(WQ(qs, 0) + d) = v4u{X.w_word[k] | (v.n << 24), X.w_ev[k], X.w_first[k], v.len};
+#pragma unroll
+              for (int q2 = 0; q2 < (kDeweyPairs + 1) / 2; q2++)
+                if ((uint32_t)(2 * q2) < v.n)
+                  *(WQ(qs, 1 + q2) + d) = v4u{(uint32_t)v.v[2 * q2], v.c[2 * q2],
+                                              2 * q2 + 1 < kDeweyPairs ? (uint32_t)v.v[2 * q2 + 1] : 0u,
+                                              2 * q2 + 1 < kDeweyPairs ? v.c[2 * q2 + 1] : 0u};
+              reinterpret_cast<uint32_t*>(WQ(qs, kWalkQuads - 1) + d)[0] = j_o;
+            }
+          }
+      }
+      // ---- puts, one stage key at a time: the key's first putter makes the node (or appends to
+      // the one an earlier page made), every putter takes a pointer linked to the next putter's
+#pragma unroll
+      for (uint32_t sk = 0; sk < (uint32_t)kMaxStageKeys; sk++) {
+        if (!((Q::kCoopSkMask >> sk) & 1u)) continue;
+        bool has = false;
+        uint32_t slot = 0;
+#pragma unroll
+        for (int k = 0; k < X_t::kP; k++)
+          if (full && (uint32_t)k < X.np && X.p_sk[k] == sk) {
+            has = true;
+            slot = (uint32_t)k;
+          }
+        const uint64_t B = __ballot(has);
+        const uint64_t Bs = B & wseg;
+        const bool first = has && !(Bs & lanes_below(lane));
+        const uint32_t exn = __shfl(nodeJ[sk], o, 64), ext = __shfl(tailJ[sk], o, 64);
+        const uint32_t cf_o = __shfl(cur_first, o, 64);
+        uint32_t nd = CEP_NONE, pr = CEP_NONE;
+        if (has) {
+          if (first && exn == CEP_NONE) {
+            nd = pool_take(A.node_pool, ncur, nend);
+            if (nd == CEP_NONE) retry = true;
+            else pr = kPred0 | nd;
+          } else {
+            pr = pool_take(A.pred_pool, pcur, pend);
+            if (pr == CEP_NONE) retry = true;
+          }
+        }
+        const uint32_t mine = first ? (exn != CEP_NONE ? exn : nd) : CEP_NONE;
+        const uint32_t node = __shfl(mine, low_lane(Bs, lane), 64);
+        const uint64_t above = Bs & ~lanes_below(lane + 1);
+        const uint32_t nxt0 = __shfl(pr, low_lane(above, lane), 64);
+        const uint32_t last = __shfl(pr, high_lane(Bs, lane), 64);
+        if (has && !retry && node != CEP_NONE) {
+          const uint32_t nxt = above ? nxt0 : CEP_NONE;
+#pragma unroll
+          for (int k = 0; k < X_t::kP; k++)
+            if ((uint32_t)k == slot) {
+              write_pred(pr, X.p_prev[k], X.p_ver[k], nxt);
+              X.p_node[k] = node;
+            }
+          if (first) {
+            const uint32_t cnt = (uint32_t)__popcll(Bs);
+            if (exn == CEP_NONE) {  // a new node at event j holding the key's putters' pointers
+              *NQ(node, 0) = v4u{j_o, 1u, pr, last};
+              *NQ(node, 1) = v4u{cf_o, sk | 0x100u | (cnt << 16), 0u, key_o};
+            } else {  // appended to the node an earlier page made
+              PR(ext).next = pr;
+              Node& n = A.nodes[node];
+              n.tail = last;
+              n.meta += cnt << 16;
+            }
+          }
+        }
+        // owner role: the key's node of (sk, j), its last pointer, its chain of event j
+        const uint64_t Bo = B & oseg;
+        const uint32_t on = __shfl(mine, low_lane(Bo, lane), 64);
+        const uint32_t ot = __shfl(pr, high_lane(Bo, lane), 64);
+        if (Bo) {
+          if (nodeJ[sk] == CEP_NONE && on != CEP_NONE) cur_first = on;
+          nodeJ[sk] = on;
+          tailJ[sk] = ot;
+        }
+      }
+      // ---- records: slots in the owner's next queue half, in record order
+      const uint32_t no = full ? X.no : 0u;
+      const uint32_t oi = wave_incl_scan(no);
+      const uint32_t ob0 = __shfl(oi, wlo ? wlo - 1 : 0, 64);
+      const uint32_t ocount_o = __shfl(ocount, o, 64);
+      const uint32_t slot0 = ocount_o + oi - no - (wlo ? ob0 : 0u);
+      uint32_t nfin = 0;
+      if (no) {
+        if (slot0 + no > A.rcap) {
+          retry = true;
+          if (A.full) atomicOr(A.full, 1u);
+        } else {
+#pragma unroll
+          for (int k = 0; k < X_t::kO; k++)
+            if ((uint32_t)k < no) {
+              uint32_t nd = X.o_node[k];
+#pragma unroll
+              for (int k2 = 0; k2 < X_t::kP; k2++)
+                if (nd == (kTok | (uint32_t)k2)) nd = X.p_node[k2];
+              store_head(h_o ^ 1u, slot0 + (uint32_t)k, X.o_stage[k], X.o_event[k], X.o_ef[k], X.o_ver[k], nd, d, rb_o);
+              store_folds(h_o ^ 1u, slot0 + (uint32_t)k, X.o_fold[k], X.o_nm[k], d, rb_o);
+              if (X.o_stage[k] & kRecFinal) nfin++;
+            }
+        }
+      }
+      // ---- the owner's key after the page: counts, errors
+      const uint64_t rb = __ballot(retry), cb = __ballot(conflict);
+      const uint32_t olo = low_lane(oseg, lane), ohi = high_lane(oseg, lane);
+      const uint32_t fi = wave_incl_scan(nfin);
+      const uint32_t t_lo_o = __shfl(oi, olo ? olo - 1 : 0, 64), t_hi_o = __shfl(oi, ohi, 64);
+      const uint32_t w_lo_o = __shfl(wi, olo ? olo - 1 : 0, 64), w_hi_o = __shfl(wi, ohi, 64);
+      const uint32_t f_lo_o = __shfl(fi, olo ? olo - 1 : 0, 64), f_hi_o = __shfl(fi, ohi, 64);
+#if CEP_PUT_LOG
+      const uint32_t s_lo_o = __shfl(si, olo ? olo - 1 : 0, 64), s_hi_o = __shfl(si, ohi, 64);
+#endif
+      const uint64_t eo = eb & oseg;
+      const uint32_t ecode = __shfl((uint32_t)X.err, low_lane(eo, lane), 64);
+      if (oseg) {
+        ocount += t_hi_o - (olo ? t_lo_o : 0u);
+        const uint32_t wn = w_hi_o - (olo ? w_lo_o : 0u);
+        wq_n += wn;
+        opc += wn;
+        n_final += f_hi_o - (olo ? f_lo_o : 0u);
+#if CEP_PUT_LOG
+        pl_n += s_hi_o - (olo ? s_lo_o : 0u);
+#endif
+        if (err == KE_OK) {
+          if ((rb | cb) & oseg) err = A.carry ? KE_CAPACITY : ((rb & oseg) ? KE_RETRY : KE_CONFLICT);  // (a stream cannot re-run a key)
+          else if (eo) err = (int)ecode;
+        }
+      }
+    }
+  }
+
   // ---------------------------------------------------------------- the key's stream
   // Lanes of a wavefront advance in lockstep; a lane whose queue holds only the begin run
   // (whose single BEGIN edge did not match) is in the reference's quiet state: an event
@@ -1132,9 +1425,12 @@ struct Lane {
   int pa_err = KE_OK;       // an exception of the per-event step (walks queued before it go first)
   uint32_t pa_seq = 0;
 
-  __device__ __forceinline__ bool tick() {
+  // tick_pre: the quiet skip, then this tick's event: 2 an event at jj (j set, its fields
+  // loaded; `known`: the begin predicate already found true), 1 no event this tick (a quiet
+  // chunk scanned), 0 the events are over or the quiet scan threw (pa_err).
+  __device__ __forceinline__ int tick_pre(bool& known) {
     CEP_PT(tq0);
-    bool known = false;
+    known = false;
     if (q.quiet && A.bhits && only_begin()) {
       // the next event whose begin predicate holds or throws, 64 positions per word;
       // event() evaluates the predicate there itself (its exception, in order)
@@ -1148,12 +1444,12 @@ struct Lane {
       }
       if (jj >= jn) {
         jj = jn;
-        return false;
+        return 0;
       }
       jj += (uint32_t)__builtin_ctzll(w);
       if (jj >= jn) {
         jj = jn;
-        return false;
+        return 0;
       }
     } else if (q.quiet && only_begin()) {
       const uint32_t lim = (jn - jj > kQuietChunk) ? jj + kQuietChunk : jn;
@@ -1161,11 +1457,11 @@ struct Lane {
       if (err) {
         pa_err = err;
         pa_seq = h;
-        return false;
+        return 0;
       }
       if (h >= lim) {
         jj = lim;
-        return jj < jn;
+        return jj < jn ? 1 : 0;
       }
       jj = h;
       known = true;  // the scan already found the begin predicate true
@@ -1177,7 +1473,11 @@ struct Lane {
       q.load_ev(ev, base + jj);
       ev_pos = jj;
     }
-    event(known);
+    return 2;
+  }
+
+  // after the event at jj: false once the events are over or the step threw (pa_err)
+  __device__ __forceinline__ bool tick_post() {
     if (err) {
       pa_err = err;
       pa_seq = jj;
@@ -1185,6 +1485,14 @@ struct Lane {
     }
     jj++;
     return jj < jn;
+  }
+
+  __device__ __forceinline__ bool tick() {
+    bool known = false;
+    const int st = tick_pre(known);
+    if (st != 2) return st == 1;
+    event(known);
+    return tick_post();
   }
 
   // the step's exception, after the final drain found nothing earlier (drained: flush() ran)
@@ -1195,7 +1503,10 @@ struct Lane {
     }
   }
 
-  // the whole key in one go (streaming sessions: one key per lane and launch)
+  // the whole key in one go (streaming sessions and single queries: one key per lane and
+  // launch).  Convergent: every lane of the wave takes each iteration (a lane whose events are
+  // over idles in it, as SIMT execution would mask it), so the flushes' cross-lane operations
+  // see the whole wave.
   __device__ __forceinline__ void run() {
     CEP_PT(tr0);
 #ifdef CEP_PROF
@@ -1205,23 +1516,48 @@ struct Lane {
     jn = j0 + n_ev;
     pa_err = KE_OK;
     bool more = jj < jn;
-    while (more) {
-      CEP_PACC(8, 1);
+#ifdef CEP_HOST_LANES
+    const bool coop = Q::kCoop && A.defer && !cep_host_single_lane();  // (tests/lane_cpu: whole waves only)
+#else
+    const bool coop = Q::kCoop && A.defer;  // (wave-uniform)
+#endif
+    (void)coop;
+    while (__any(more)) {
+      CEP_PACC(8, more ? 1 : 0);
       CEP_PT(tf0);
-      if (A.defer && __any(wq_n >= kWalkFlush || pl_n + plog_margin() > kPutLog)) {
-        flush(pl_n + plog_margin() <= kPutLog);
-        if (err) break;
+      if (A.defer && __any(more && (wq_n >= kWalkFlush || pl_n + plog_margin() > A.plog))) {
+        flush(pl_n + plog_margin() <= A.plog, more);
+        if (more && err) more = false;  // a walk threw: the key stops there
       }
       CEP_PT(tf1);
       CEP_PACC(0, tf1 - tf0);
-      more = tick();
+      if constexpr (Q::kCoop) {
+        if (coop) {  // the records of the wave's events stepped together (nfa_coop.h)
+          bool known = false;
+          const int st = more ? tick_pre(known) : 0;
+          const bool act = st == 2;
+          if (act) event_pre();
+          coop_records(act);
+          if (act) {
+            if (!err) event_post(known);
+            more = tick_post();
+          } else {
+            more = st == 1;
+          }
+        } else if (more) {
+          more = tick();
+        }
+      } else if (more) {
+        more = tick();
+      }
     }
     CEP_PT(tr1);
-    if (pa_err != KE_OK || !err) {
-      err = KE_OK;
-      flush();  // every lane of the wave together
-      finish_err();
-    }
+    // the final drain, every lane of the wave together (lanes whose walk threw mid-stream take
+    // part with nothing to walk)
+    const bool fin = pa_err != KE_OK || !err;
+    if (fin) err = KE_OK;
+    flush(false, fin);
+    if (fin) finish_err();
 #ifdef CEP_PROF
     CEP_PT(tr2);
     CEP_PACC(5, tr2 - tr1);
@@ -1321,7 +1657,7 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
   const uint32_t lane = threadIdx.x & 63;
   Lane<F, Q> L(A, q);
   L.rb = reinterpret_cast<v4u*>(A.rings) + (slot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + lane;
-  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap) + lane;
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap, A.plog) + lane;
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + lane;
   bool has = false, drained = false;
@@ -1369,11 +1705,11 @@ __device__ __forceinline__ void run_jobs(const NfaArgs& A, Q& q, v4u* lds) {
     // lane has events left to run (the finished lanes' drains batched into one flush)
     const uint64_t ending = __ballot(has && phase == 1);
     CEP_PT(tf0);
-    if (A.defer && (__any(has && (L.wq_n >= kWalkFlush || L.pl_n + L.plog_margin() > kPutLog)) ||
+    if (A.defer && (__any(has && (L.wq_n >= kWalkFlush || L.pl_n + L.plog_margin() > A.plog)) ||
                     (ending && (__popcll(ending) >= kJobDrain || !__any(has && phase == 0))))) {
       // every lane of the wave together (lanes without a queue leave at once); lanes at their
       // job's end drain all of theirs
-      L.flush(has && phase == 0 && L.pl_n + L.plog_margin() <= kPutLog);
+      L.flush(has && phase == 0 && L.pl_n + L.plog_margin() <= A.plog);
       if (has && phase == 0 && L.err) phase = 2;  // a walk threw mid-job: the job stops there
       if (has && phase == 1) {
         L.finish_err();
@@ -1427,10 +1763,13 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   }
 #endif
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t job;
+  // A lane without a job stays in its wave with no events (has false): the wave-wide loops and
+  // the coop pages' shuffles (nfa_coop.h) read every lane of the wave, so none may have left.
+  bool has = true;
+  uint64_t job = 0;
   if (A.jobs) {
-    if (slot >= A.n_jobs) return;
-    job = A.jobs[slot];
+    if (slot >= A.n_jobs) has = false;
+    else job = A.jobs[slot];
   } else {
     const uint32_t nq = A.n_q ? A.n_q : 1;
     const uint64_t w = slot / 64;
@@ -1440,33 +1779,36 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     const uint64_t l = slot % 64;
     const uint64_t rank = A.spread ? l * A.spread + ((A.spread_snake && (l & 1)) ? A.spread - 1 - w : w)
                                    : (w / nq) * 64 + l;
-    if (rank >= A.n_keys) return;
-    job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
+    if (rank >= A.n_keys) has = false;
+    else job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
   }
+  if (!__any(has)) return;  // (the whole wave)
   const uint32_t qi = (uint32_t)(job / A.n_keys);
   const uint32_t key = (uint32_t)(job % A.n_keys);
   q.set_query(qi);
   Lane<F, Q> L(A, q);
   L.key = key;
-  L.n_ev = (uint32_t)(A.key_off[key + 1] - A.key_off[key]);
+  L.n_ev = has ? (uint32_t)(A.key_off[key + 1] - A.key_off[key]) : 0u;
   // a stream's run queue lives at its key's position (kept from batch to batch whatever lane
   // order the batch runs in); a per-batch launch's at the lane's slot (coalesced)
   const uint64_t rslot = A.carry ? job : slot;
   L.rb = reinterpret_cast<v4u*>(A.rings) +
          (rslot / 64) * (2ull * A.rcap * Lane<F, Q>::Lay::kQuads * 64) + (rslot % 64);
-  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap) + (slot % 64);
+  L.wb = reinterpret_cast<v4u*>(A.walks) + (slot / 64) * walkq_group_quads(A.wcap, A.plog) + (slot % 64);
   if (Lane<F, Q>::kRL > 0)  // (kRL == 0: never dereferenced)
     L.lr = (lds_v4u*)lds + (threadIdx.x / 64) * (2 * Lane<F, Q>::kRL * Lane<F, Q>::Lay::kLdsQuads * 64) + (threadIdx.x % 64);
   KeyState& ks = A.ks[job];
-  KeyCarry* kc = A.carry ? A.carry + job : nullptr;
+  KeyCarry* kc = (A.carry && has) ? A.carry + job : nullptr;
+  if (kc && kc->live && kc->err) {  // stopped by an exception: stays stopped
+    ks.n_matches = ks.n_pairs = 0;
+    ks.out_first = CEP_NONE;
+    ks.err = kc->err;
+    ks.err_seq = kc->err_seq;
+    has = false;
+    kc = nullptr;
+    L.n_ev = 0;
+  }
   if (kc && kc->live) {  // the key's NFA as the previous batch left it
-    if (kc->err) {        // stopped by an exception: stays stopped
-      ks.n_matches = ks.n_pairs = 0;
-      ks.out_first = CEP_NONE;
-      ks.err = kc->err;
-      ks.err_seq = kc->err_seq;
-      return;
-    }
     L.j0 = kc->seq;
     L.half = kc->half;
     L.count = kc->count;
@@ -1483,7 +1825,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     L.bdig = 1;
     L.half = 0;
     L.count = 0;
-    if (!Lane<F, Q>::kBeginReg) {
+    if (!Lane<F, Q>::kBeginReg && has) {
       Dewey v;
       dw_init(v, 1);
       L.ocount = 0;
@@ -1493,8 +1835,9 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
       L.count = 1;
     }
   }
-  L.base = A.key_off[key] - L.j0;
+  L.base = has ? A.key_off[key] - L.j0 : 0;
   L.run();
+  if (!has) return;
   ks.n_matches = L.n_matches;
   ks.n_pairs = L.n_pairs;
   ks.out_first = L.out_first;

@@ -43,11 +43,10 @@ struct HipError : std::runtime_error {
   } while (0)
 
 // A grow-only device buffer.
-// $CEP_HOST_TRACE (measurement runs): device (re)allocations and push phases on stderr, ms
-static bool host_trace() {
-  static const bool on = std::getenv("CEP_HOST_TRACE") != nullptr;
-  return on;
-}
+// $CEP_HOST_TRACE (measurement runs, Tuning.host_trace): device (re)allocations and push phases
+// on stderr, ms.  Set when a session is created with the knob.
+static bool g_host_trace = false;
+static bool host_trace() { return g_host_trace; }
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -211,6 +210,7 @@ struct GroupRt {
 struct cep_session {
   int device = 0;
   cep_opts opts{};
+  cep::Tuning tune{};  // measurement knobs, read once at creation (tuning.cpp)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   int cus = 256;  // compute units of the device (persistent-lane grids)
@@ -299,8 +299,10 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint64_t nk = s->n_keys;
   const uint64_t n_tiles = stencil_tiles(s->n_events);
   const uint64_t n_groups = n_tiles / 64 + 2;
-  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));                          // tile counts
-  s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
+  // counters, then group counts, group completions, the start ticket and the tile counts: one
+  // region, zeroed by the key-index pass before the stencil launch
+  const uint64_t n_zero = (sizeof(Scratch) + sizeof(uint32_t) * (2 * n_groups + 1 + n_tiles + 1)) / 4 + 1;
+  s->status.ensure(4 * n_zero);
   s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
   s->bnd.ensure(sizeof(uint32_t) * (s->n_events / 64 + 2));                       // word -> key
@@ -347,8 +349,10 @@ void run_stencil(cep_session* s, QueryRt& r) {
   }
   for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
-  a.tile_cnt = s->tile_key.as<uint32_t>();
   a.group_cnt = reinterpret_cast<uint32_t*>(sc + 1);
+  a.group_done = a.group_cnt + n_groups;
+  a.ticket = a.group_done + n_groups;
+  a.tile_cnt = a.ticket + 1;
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
   a.total = &sc->total;
@@ -360,12 +364,12 @@ void run_stencil(cep_session* s, QueryRt& r) {
   // (4 % of this 0.12 ms step), so the 4 us key-index pass is not timed (aux_ms 0).
   // wave_keys also zeroes the counters (no memset launch); no D2H copy of them either
   HIPCHECK(launch_wave_keys(s->key_off, nk, s->n_events, s->keylist.as<uint32_t>(), reinterpret_cast<uint32_t*>(sc),
-                            (uint32_t)((sizeof(Scratch) + sizeof(uint32_t) * n_groups) / 4), s->stream));
+                            (uint32_t)n_zero, s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][1], s->stream));
-  HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->stream));
+  HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->tune.stencil_pf, s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][2], s->stream));
   r.pending = true;
-  r.launches = 2;  // stencil_mask + stencil_emit
+  r.launches = 1;  // stencil_fused (mask and emit roles)
   r.digest_valid = false;
   r.arity = m;
   // no per-key errors on this path: the predicates and folds are total
@@ -436,8 +440,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // waves per CU of the JIT kernels (compile.cpp): the narrow build 3 per SIMD, the wide one
   // (streams, re-runs) 2; $CEP_RESIDENT_WAVES (per CU): measurement runs
   uint64_t waves_cu = streaming ? 8 : 12, waves_cu_wide = 8;
-  if (const char* e = std::getenv("CEP_RESIDENT_WAVES"))
-    if (std::atoi(e) > 0) waves_cu = waves_cu_wide = (uint64_t)std::atoi(e);
+  if (s->tune.resident_waves > 0) waves_cu = waves_cu_wide = s->tune.resident_waves;
   const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
   const uint64_t resident_wide = (uint64_t)s->cus * waves_cu_wide * 64;
   auto grid_for = [&](uint64_t n) { return std::min<uint64_t>((n + 255) / 256 * 256, resident); };
@@ -446,7 +449,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // their longest-first lane order already balances the waves (persistent lanes cost cfg 3
   // ~35 %), and their narrow kernel is built without the persistent driver; groups mix light
   // and heavy queries.
-  const bool persist = !streaming && !std::getenv("CEP_NO_PERSIST") && Q > 1;
+  const bool persist = !streaming && !s->tune.no_persist && Q > 1;
   // An underfilled single-query launch (fewer waves than the chip holds: a shard of a
   // multi-GPU run, a small batch) is as long as its longest wave, whose length is its heaviest
   // key's chain of events times the wave's per-event cost; that cost grows with the number of
@@ -457,8 +460,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // $CEP_SPREAD: 0 off, 1 rows in order, 2 (default) odd lanes reversed - measurement runs)
   uint32_t snake = 0;
   if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64) {
-    const char* e = std::getenv("CEP_SPREAD");
-    const int mode = e ? std::atoi(e) : 2;
+    const int mode = s->tune.spread;
     if (mode != 0) spread = std::min<uint64_t>(resident / 64, nk);
     snake = mode == 2 ? 1u : 0u;
   }
@@ -474,10 +476,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // (persistent lanes keep their ranges across jobs) take bigger ranges; streams hold a range
   // per key between batches, so theirs stay small
   uint32_t nchunk = streaming ? 16 : 64, ochunk = streaming ? 1 : 8;
-  if (const char* e = std::getenv("CEP_NODE_CHUNK"))  // (measurement runs)
-    if (std::atoi(e) > 0) nchunk = (uint32_t)std::atoi(e);
-  if (const char* e = std::getenv("CEP_OUT_CHUNK"))
-    if (std::atoi(e) > 0) ochunk = (uint32_t)std::atoi(e);
+  if (s->tune.node_chunk) nchunk = s->tune.node_chunk;  // (measurement runs)
+  if (s->tune.out_chunk) ochunk = s->tune.out_chunk;
   const uint32_t pchunk = nchunk;
   const uint64_t ev_q = (uint64_t)((double)s->n_events * (double)Q);
   // (the last batch's pool tops already count the ranges lanes held at its end; the estimate
@@ -497,14 +497,17 @@ void run_nfa(cep_session* s, GroupRt& g) {
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
   s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
-  // deferred walks a key can queue (nfa_lane.h drains at CEP_WALK_FLUSH; $CEP_WALK_CAP: tuning)
+  // deferred walks a key can queue (nfa_lane.h drains at the compiled CEP_WALK_FLUSH, the
+  // same value as tune.walk_flush; $CEP_WALK_CAP: tuning)
   // (a stream cannot re-run a key whose event overflows its queue: room for every walk one
   // event can queue - removePattern and branch walks of its records, one extraction per output
   // - beyond the drain threshold)
-  uint32_t wcap = streaming ? std::max<uint32_t>(64, 24 + 3 * rcap) : 64;
-  if (const char* e = std::getenv("CEP_WALK_CAP"))
-    if (std::atoi(e) > 0) wcap = (uint32_t)std::atoi(e);
-  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap));
+  uint32_t wcap = streaming ? std::max<uint32_t>(64, s->tune.walk_flush + 3 * rcap) : 64;
+  if (s->tune.walk_cap) wcap = s->tune.walk_cap;
+  // put-log entries per lane: every put one event can log fits twice over (a stream turns a
+  // put-log overflow into a sticky error, so it must never happen there)
+  uint32_t plog = put_log_entries(rcap);
+  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap, plog));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
@@ -557,6 +560,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.rcap = rcap;
   a.walks = s->walks.p;
   a.wcap = wcap;
+  a.plog = plog;
   a.defer = 1;
   a.n_q = (uint32_t)Q;
   a.spread = spread;
@@ -576,7 +580,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   if (persist) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
-    if (const char* e = std::getenv("CEP_JOB_MAP")) a.job_map = (uint32_t)std::atoi(e);  // (measurement runs)
+    a.job_map = s->tune.job_map;  // (measurement runs)
     // Heavy-first ($CEP_HEAVY_FIRST, opt-in): when the last batch's output was concentrated in
     // a few queries (config 5: the 8 variants with the loosest dip predicate emit ~95 % of the
     // event ids), their jobs go first.  Measured slower on config 5 (4.55 / 3.94 s against
@@ -584,7 +588,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     // than the key-major waves, whose light lanes keep claiming jobs beside the heavy ones.
     // Results do not depend on the order.
     const uint32_t nh = heavy_queries(g.qwork, g.qmap_h);
-    if (nh > 0 && std::getenv("CEP_HEAVY_FIRST")) {
+    if (nh > 0 && s->tune.heavy_first) {
       g.qmap.ensure(4 * Q);
       HIPCHECK(hipMemcpyAsync(g.qmap.p, g.qmap_h.data(), 4 * Q, hipMemcpyHostToDevice, s->stream));
       a.qmap = g.qmap.as<uint32_t>();
@@ -636,7 +640,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   } else {
     g.est_valid = false;
   }
-  const bool prof = std::getenv("CEP_PROF") != nullptr;  // (the query must be compiled with it too)
+  const bool prof = s->tune.prof;  // (the query must be compiled with it too)
   if (prof) {
     s->prof.ensure(16 * sizeof(unsigned long long));
     HIPCHECK(hipMemsetAsync(s->prof.p, 0, 16 * sizeof(unsigned long long), s->stream));
@@ -645,8 +649,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   HIPCHECK(hipEventRecord(s->ev2, s->stream));
   // ($CEP_STREAM_NARROW: a stream on the narrow build - no put log, so a walk conflict is a sticky
   // error - and $CEP_STREAM_NO_ORDER: without the lane order; measurement runs only)
-  static const bool stream_narrow = std::getenv("CEP_STREAM_NARROW") != nullptr;
-  if (streaming && std::getenv("CEP_STREAM_NO_ORDER")) a.order = nullptr;
+  const bool stream_narrow = s->tune.stream_narrow;
+  if (streaming && s->tune.stream_no_order) a.order = nullptr;
   HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
@@ -738,7 +742,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
     while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
     a.rcap = rcap;
     s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
-    s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap));  // (may move: re-read below)
+    plog = put_log_entries(rcap);
+    a.plog = plog;
+    s->walks.ensure(walkq_size(std::max<uint64_t>(most, 1), wcap, plog));  // (may move: re-read below)
     a.rings = s->retry_rings.p;
     a.walks = s->walks.p;
     a.order = nullptr;
@@ -938,6 +944,8 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
   }
   auto s = std::make_unique<cep_session>();
   if (opts) s->opts = *opts;
+  s->tune = cep::tuning_from_env();  // (the only read of the measurement knobs: not per launch)
+  if (s->tune.host_trace) g_host_trace = true;
   for (int i = 0; i < n_queries; i++)
     if (queries[i]->windowed && s->opts.tier != CEP_TIER_JIT)
       return fail(CEP_E_INVALID, "semantic WITHIN runs on the JIT tier only");
@@ -1168,7 +1176,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     s->watermark = INT64_MIN;
     s->wm_pending = false;
     s->wm_fold = s->ts && s->n_events && !s->groups.empty() && s->groups[0]->fn_bits && s->groups[0]->fn_est &&
-                 s->n_keys > 64 && !std::getenv("CEP_NO_WM_FOLD");
+                 s->n_keys > 64 && !s->tune.no_wm_fold;
     if (s->ts && s->n_events && !s->wm_fold) {  // read back with the batch's other results (resolve())
       s->scratch.ensure(sizeof(Scratch));
       Scratch* sc = s->scratch.as<Scratch>();
@@ -1339,7 +1347,10 @@ int cep_watermark(cep_session* s, int64_t* out) {
 // stream exactly (tests/test_gpu_parity.py::test_streaming_snapshot_restore).
 namespace {
 constexpr uint64_t kSnapMagic = 0x31504E5350454300ull;  // "\0CEPSNP1"
-constexpr uint32_t kSnapVersion = 2;  // 2: a node's first pointer in its own slot (preds0)
+constexpr uint32_t kSnapVersion = 3;
+// 2: a node's first pointer in its own slot (preds0).  3: a run record's header w field holds
+// its node hint (was the Dewey length, now the sum of the pair counts), and Node quad 1's w
+// field holds the key (cep_live_floor)
 
 uint64_t query_fingerprint(const cep_query* q) {
   uint64_t h = 1469598103934665603ull;

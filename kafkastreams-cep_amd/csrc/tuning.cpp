@@ -1,0 +1,48 @@
+// tuning.cpp — the measurement knobs of libcep ($CEP_* environment variables), read in one
+// place: at session creation (cep_session_create keeps a copy in the session) and, for the
+// knobs compiled into a query's kernel, at query compile.  Nothing on the launch path reads
+// the environment (tests/test_native_abi.py checks the sources).  Results never depend on
+// these knobs.
+#include <cstdlib>
+
+#include "cep_internal.h"
+
+namespace cep {
+
+namespace {
+bool flag(const char* name) { return std::getenv(name) != nullptr; }
+long num(const char* name, long dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atol(e) : dflt;
+}
+}  // namespace
+
+uint32_t tuning_walk_flush() {
+  const long v = num("CEP_WALK_FLUSH", 24);
+  return v > 0 ? (uint32_t)v : 24u;
+}
+
+Tuning tuning_from_env() {
+  Tuning t;
+  const long rw = num("CEP_RESIDENT_WAVES", 0);
+  t.resident_waves = rw > 0 ? (uint32_t)rw : 0u;
+  t.no_persist = flag("CEP_NO_PERSIST");
+  t.spread = (int)num("CEP_SPREAD", 2);
+  const long nc = num("CEP_NODE_CHUNK", 0), oc = num("CEP_OUT_CHUNK", 0), wc = num("CEP_WALK_CAP", 0);
+  t.node_chunk = nc > 0 ? (uint32_t)nc : 0u;
+  t.out_chunk = oc > 0 ? (uint32_t)oc : 0u;
+  t.walk_cap = wc > 0 ? (uint32_t)wc : 0u;
+  t.walk_flush = tuning_walk_flush();
+  t.job_map = (uint32_t)num("CEP_JOB_MAP", 0);
+  t.heavy_first = flag("CEP_HEAVY_FIRST");
+  t.prof = flag("CEP_PROF");
+  t.stream_narrow = flag("CEP_STREAM_NARROW");
+  t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
+  t.no_wm_fold = flag("CEP_NO_WM_FOLD");
+  const long pf = num("CEP_STENCIL_PF", 0);
+  t.stencil_pf = (pf == 1 || pf == 2 || pf == 4) ? (int)pf : 0;
+  t.host_trace = flag("CEP_HOST_TRACE");
+  return t;
+}
+
+}  // namespace cep

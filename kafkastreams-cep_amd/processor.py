@@ -40,15 +40,22 @@ numbers of every key) and the retained records - is written to the `_cep_nfa` st
 (topic, partition) as the reference keys it, at every commit (`punctuate`, `close`), and
 reloaded in `init`.  Records processed after the last commit are replayed by the host after a
 restart (Kafka's at-least-once delivery), so a processor recreated from the store forwards
-exactly what one uninterrupted processor would.  The store is whatever `context.get_state_store
-("_cep_nfa")` returns (any mutable mapping; a real host passes its persistent store), or the
-`store` argument.
+exactly what one uninterrupted processor would.  This commit granularity is a deliberate
+difference from the reference's per-record store write (it would serialise every key's NFA per
+record); the results forwarded are the same.  The store is whatever
+`context.get_state_store("_cep_nfa")` returns (any mutable mapping; a real host passes its
+persistent store), or the `store` argument.  The blob is a versioned plain encoding (no
+pickle): the device snapshot's own binary format, then a JSON document of the retained records
+whose keys and values go through `key_serde` / `value_serde` (Kafka-style serdes:
+`serialize(obj) -> bytes`, `deserialize(bytes) -> obj`; the default is JSON, for keys and
+values that are JSON data - the README's StockEvent dicts, strings, numbers).
 
 There is no CPU matching path: without libcep.so and a GPU, `init()` raises.
 """
 from __future__ import annotations
 
-import pickle
+import base64
+import json
 
 import numpy as np
 
@@ -88,7 +95,26 @@ class CapacityError(JavaException):
 _EXC = {1: NullPointerException, 2: IllegalStateException, 3: ArithmeticException, 16: CapacityError}
 
 NFA_STATES_STORE = "_cep_nfa"  # CEPProcessor.java:56
-_CKPT_MAGIC = b"CEPPROC1"
+_CKPT_MAGIC = b"CEPPROC2"  # 2: plain encoding (JSON host half); 1 (pickle) is not read
+_CKPT_VERSION = 2
+
+
+class JsonSerde:
+    """The default key/value serde of the processor's checkpoint: JSON data (dicts, lists,
+    strings, numbers, booleans, None).  Anything else needs a serde of its own (the reference's
+    Kryo serde likewise accepts only registered classes, serde/KryoSerDe.java)."""
+
+    @staticmethod
+    def serialize(obj) -> bytes:
+        try:
+            return json.dumps(obj, separators=(",", ":"), allow_nan=False).encode()
+        except (TypeError, ValueError) as e:
+            raise TypeError(f"cannot checkpoint {type(obj).__name__} values as JSON: pass key_serde/"
+                            f"value_serde to CEPProcessor") from e
+
+    @staticmethod
+    def deserialize(data: bytes):
+        return json.loads(data.decode())
 
 
 # ---- Event / Sequence ---------------------------------------------------------------------
@@ -213,13 +239,16 @@ class CEPProcessor:
 
     def __init__(self, pattern, in_memory: bool = False, *, batch_size: int = 4096,
                  max_keys: int = 1 << 16, device: int = 0, session_factory=None, semantic_within: bool = False,
-                 store=None):
+                 store=None, key_serde=None, value_serde=None):
         """semantic_within: enforce the query's WITHIN on the record timestamps (this build's
         semantic mode, Pattern.to_ir(semantic_within=True)); the default is the reference's
         behaviour, where WITHIN never prunes.  in_memory=False (the reference's default): the
         state is checkpointed to the `_cep_nfa` store at every commit and reloaded by init();
-        `store` overrides the context's store."""
+        `store` overrides the context's store; key_serde / value_serde encode the retained
+        records' keys and values in the checkpoint (default JsonSerde)."""
         self.pattern = pattern
+        self.key_serde = key_serde or JsonSerde
+        self.value_serde = value_serde or JsonSerde
         self.in_memory = in_memory  # the reference's store choice (CEPProcessor.java:144-149)
         self._store = store
         self.batch_size = max(1, int(batch_size))
@@ -279,26 +308,42 @@ class CEPProcessor:
 
     def checkpoint(self) -> bytes:
         """The processor's whole state as one blob: the device session's snapshot (every key's
-        NFA) and the retained records with their per-key sequence numbers."""
+        NFA) and the retained records with their per-key sequence numbers.  Layout: magic
+        "CEPPROC2", u64 length + the session snapshot, then UTF-8 JSON {version, max_keys, ir
+        (hex), keys, base, total, events} where keys and values are base64 of their serde's
+        bytes and an event is [timestamp, topic, partition, offset, value]."""
         dev = self.session.snapshot()
-        host = pickle.dumps({"keys": self._keys, "events": self._events, "base": self._ev_base,
-                             "total": self._ev_total, "max_keys": self.max_keys, "ir": self.ir},
-                            protocol=pickle.HIGHEST_PROTOCOL)
-        return _CKPT_MAGIC + len(dev).to_bytes(8, "little") + dev + host
+        b64 = lambda b: base64.b64encode(b).decode()  # noqa: E731
+        ks, vs = self.key_serde, self.value_serde
+        host = {"version": _CKPT_VERSION, "max_keys": self.max_keys, "ir": self.ir.hex(),
+                "keys": [b64(ks.serialize(k)) for k in self._keys],
+                "base": [int(x) for x in self._ev_base], "total": [int(x) for x in self._ev_total],
+                "events": [[[e.timestamp, e.topic, e.partition, e.offset, b64(vs.serialize(e.value))] for e in evs]
+                           for evs in self._events]}
+        hb = json.dumps(host, separators=(",", ":")).encode()
+        return _CKPT_MAGIC + len(dev).to_bytes(8, "little") + dev + hb
 
     def restore(self, blob: bytes) -> None:
-        """Loads a checkpoint() blob written by a processor over the same pattern (the
-        processor's own store data; never a file from elsewhere)."""
+        """Loads a checkpoint() blob written by a processor over the same pattern.  Nothing in
+        the blob is executed: the host half is JSON data, decoded by the serdes."""
         if blob[:8] != _CKPT_MAGIC:
-            raise ValueError("not a CEPProcessor checkpoint")
+            raise ValueError("not a CEPProcessor checkpoint (or an older, unsupported version)")
         n = int.from_bytes(blob[8:16], "little")
-        host = pickle.loads(blob[16 + n:])
-        if host["ir"] != self.ir or host["max_keys"] != self.max_keys:
+        host = json.loads(blob[16 + n:].decode())
+        if not isinstance(host, dict) or host.get("version") != _CKPT_VERSION:
+            raise ValueError("unsupported CEPProcessor checkpoint version")
+        if host["ir"] != self.ir.hex() or host["max_keys"] != self.max_keys:
             raise ValueError("checkpoint of another pattern or key space")
+        keys = [self.key_serde.deserialize(base64.b64decode(k)) for k in host["keys"]]
+        events = [[Event(k, self.value_serde.deserialize(base64.b64decode(v)), ts, topic, part, off)
+                   for ts, topic, part, off, v in evs] for k, evs in zip(keys, host["events"])]
+        if not (len(events) == len(keys) == len(host["base"]) == len(host["total"])):
+            raise ValueError("malformed CEPProcessor checkpoint")
         self.session.restore(blob[16:16 + n])
-        self._keys = list(host["keys"])
+        self._keys = keys
         self._key_ids = {k: i for i, k in enumerate(self._keys)}
-        self._events, self._ev_base, self._ev_total = host["events"], host["base"], host["total"]
+        self._events, self._ev_base, self._ev_total = events, [int(x) for x in host["base"]], \
+            [int(x) for x in host["total"]]
 
     def commit(self) -> None:
         """Writes the checkpoint into the `_cep_nfa` store (a no-op in memory)."""

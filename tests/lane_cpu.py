@@ -36,9 +36,10 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False):
     # $CEP_LANE_DEFINES="A=1 B=2": tuning knobs of nfa_lane.h for this build (tests of the knobs)
     src = "".join(f"#define {d.replace('=', ' ', 1)}\n" for d in os.environ.get("CEP_LANE_DEFINES", "").split()) + src
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
-                   ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
+                   ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_coop.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
     deps += open(os.path.join(HERE, "lane_cpu", "hip", "hip_runtime.h")).read()
+    deps += open(os.path.join(HERE, "lane_cpu", "wave_emu.h")).read()
     key = hashlib.sha1((src + deps).encode()).hexdigest()[:16]
     if key in _libs:
         return _libs[key]

@@ -12,8 +12,11 @@
 #include <vector>
 
 #include QUERY_SRC
+#include "wave_emu.h"
 
 thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
+
+static void wave_body(void* a) { cep_nfa_jit(*static_cast<cep::NfaArgs*>(a)); }
 uint64_t cep_lane_stats[9];
 extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
 
@@ -155,19 +158,25 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       rings_batch.resize(ring_bytes(8, nslots, rc) / 16 + 64);
       scribble(rings_batch.data(), rings_batch.size() * 16);
     }
-    const uint32_t wc = streaming ? std::max<uint32_t>(64, 24 + 3 * rc) : 64;  // (session.cpp run_nfa)
-    std::vector<v4u> walks(walkq_bytes(nslots, wc) / 16 + 64);
+    const uint32_t wc = streaming ? std::max<uint32_t>(64, kWalkFlush + 3 * rc) : 64;  // (session.cpp run_nfa)
+    const uint32_t pl = put_log_entries(rc);
+    std::vector<v4u> walks(walkq_bytes(nslots, wc, pl) / 16 + 64);
     scribble(walks.data(), walks.size() * 16);
     a.rings = streaming ? g_stream.rings.data() : rings_batch.data();
     a.rcap = rc;
     a.walks = walks.data();
     a.wcap = wc;
+    a.plog = pl;
     a.defer = (uint32_t)df;
     blockDim.x = 256;
-    for (uint64_t s = 0; s < nslots; s++) {
-      blockIdx.x = (unsigned)(s / 256);
-      threadIdx.x = (unsigned)(s % 256);
-      cep_nfa_jit(a);
+    if (std::getenv("CEP_LANE_WAVES")) {  // whole 64-lane waves (wave_emu.h): cross-lane ops see every lane
+      for (uint64_t s = 0; s < nslots; s += 64) emu::run_wave((unsigned)(s / 256), (unsigned)(s % 256), wave_body, &a);
+    } else {
+      for (uint64_t s = 0; s < nslots; s++) {
+        blockIdx.x = (unsigned)(s / 256);
+        threadIdx.x = (unsigned)(s % 256);
+        cep_nfa_jit(a);
+      }
     }
   };
   // $CEP_LANE_POOL: node/pred pools of that many entries for the first launch (as session.cpp

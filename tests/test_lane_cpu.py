@@ -239,3 +239,92 @@ def test_dewey_short_compat_matches_general():
                            f"-I{lane_cpu.CSRC}", os.path.join(here, "lane_cpu", "dewey_check.cpp"), "-o", exe])
     out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
     assert out.strip().endswith("bad 0") and "checked 14400" in out
+
+
+def test_lane_partial_drain_conflict_runs_earlier_walks(monkeypatch):
+    """a partial drain that finds a conflict keeps draining every walk queued
+    before the put that throws (their matches and exceptions come first in the reference).
+    Seed 21 with a 32-walk flush threshold lost such walks before the fix."""
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_PARTIAL_DRAIN=2 CEP_WALK_FLUSH=32")
+    q = random_query(21)
+    ir = q.to_ir()
+    off, cols = random_stream(21, 60, 14)
+    g = lane_cpu.run(ir, off, cols)
+    assert g["stats"]["exact_conflicts"] > 0
+    lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+
+
+@pytest.mark.parametrize("persist", [True, False])
+@pytest.mark.parametrize("case", ["stock", "any_kleene", "group", "fuzz", "stream"])
+def test_lane_whole_waves(case, persist, monkeypatch):
+    """The same lane code run as whole 64-lane waves (tests/lane_cpu/wave_emu.h: every lane a
+    fiber, each cross-lane operation a rendezvous of the wave's live lanes), so the wave-wide
+    drains, partial drains and job claiming see their real neighbours: equal to the oracle.
+    persist False: one lane per key as libcep launches single queries - the wave-cooperative
+    record pages (nfa_coop.h) step the records, as do streams."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_WAVES", "1")
+    if not persist:
+        monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
+    if case == "group":
+        cfg = W.SynthConfig("t", "stock", 40, 300, 0xCE90000 + 8)
+        off, cols = W.generate(cfg)
+        irs = [p.to_ir() for p in W.multi_queries(64)[48:64]]
+        for ir, g in zip(irs, lane_cpu.run_group(irs, off, cols)):
+            lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+        return
+    if case == "fuzz":
+        for seed in (5, 21, 80, 393):
+            ir = random_query(seed).to_ir()
+            if oracle.compile_check(ir):
+                continue
+            off, cols = random_stream(seed, 60, 14)
+            lane_cpu.assert_same(lane_cpu.run(ir, off, cols), oracle.run(ir, off, cols), off)
+        return
+    cfg = W.SynthConfig("t", "stock", 130, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = (W.any_kleene_query() if case == "any_kleene" else W.stock_query("readme")).to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    if case == "stream":
+        batches = SS.split(off, cols, 3, seed=3)
+        outs = [lane_cpu.run(ir, ko, cs, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
+        assert SS.merge(outs) == SS.oracle_per_key(r, off)
+        return
+    lane_cpu.assert_same(lane_cpu.run(ir, off, cols), r, off)
+    lane_cpu.assert_same(lane_cpu.run(ir, off, cols, narrow=True), r, off)
+
+
+@pytest.mark.parametrize("seed", [3, 21, 80, 393, 571])
+def test_lane_coop_conflicts_and_partial_drains(seed, monkeypatch):
+    """The wave-cooperative record pages (nfa_coop.h, whole waves) under forced partial drains
+    and a small drain threshold, on fuzz streams whose deferred walks conflict with later puts
+    (the put stamps come from the pages): per batch and as a stream (wide build, put log)."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_WAVES", "1")
+    monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_PARTIAL_DRAIN=2 CEP_WALK_FLUSH=4")
+    ir = random_query(seed).to_ir()
+    if oracle.compile_check(ir):
+        pytest.skip("reference compile-time exception")
+    off, cols = random_stream(seed, 60, 14)
+    r = oracle.run(ir, off, cols)
+    lane_cpu.assert_same(lane_cpu.run(ir, off, cols), r, off)
+    g = lane_cpu.run(ir, off, cols, narrow=True)  # (keys whose versions outgrow 3 pairs: capacity here)
+    ok = g["err_code"] != 16
+    np.testing.assert_array_equal(g["err_code"][ok], r["err_code"][ok])
+    batches = SS.split(off, cols, 3, seed=seed)
+    outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0)) for b, (ko, cs) in enumerate(batches)]
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
+def test_lane_coop_small_queue_retry(monkeypatch):
+    """Pages whose records overflow a 2-record run queue: the key is re-run (KE_RETRY), exact."""
+    monkeypatch.setenv("CEP_LANE_WAVES", "1")
+    monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
+    cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("test").to_ir()
+    g = lane_cpu.run(ir, off, cols, rcap=2)
+    assert g["retried"] > 0
+    lane_cpu.assert_same(g, oracle.run(ir, off, cols, threads=8), off)

@@ -96,3 +96,17 @@ def test_bad_ir_is_rejected():
         N.Query(b"CEPQ\x02\x00\x00\x00")
     with pytest.raises(N.CepError):
         N.Query(W.stock_query().to_ir() + b"\x00")
+
+
+def test_launch_path_reads_no_environment():
+    """The measurement knobs ($CEP_*) are read in one place, tuning.cpp, when a session is
+    created (and compile.cpp / jit.cpp at query compile); no source of the launch path (the
+    session's push/run code, the kernels' host launchers) calls getenv."""
+    csrc = os.path.join(ROOT, "kafkastreams-cep_amd", "csrc")
+    allowed = {"tuning.cpp", "compile.cpp", "jit.cpp"}
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".cpp", ".hip", ".h")) and f not in allowed:
+            src = re.sub(r"//.*", "", open(os.path.join(csrc, f)).read())
+            assert "getenv" not in src, f
+    ses = open(os.path.join(csrc, "session.cpp")).read()
+    assert "tuning_from_env()" in ses and ses.count("tuning_from_env") == 1

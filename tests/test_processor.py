@@ -355,3 +355,38 @@ def test_semantic_within_processor_gpu():
             ctx.send(k, v, T0 + i * gap)
         proc.close()
         assert [demo_json(s) for _, s in ctx.forwarded] == want, (semantic, gap)
+
+
+def test_checkpoint_is_plain_data():
+    """The checkpoint's host half is versioned JSON (no pickle): values go through the
+    value serde; a value the default JSON serde cannot encode asks for a serde of its own."""
+    import json
+    stores = {}
+    ctx = P.RecordContext("StockEvents", 0, stores=stores)
+    proc = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
+    proc.init(ctx)
+    for k, v, ts in _readme_records():
+        ctx.send(k, v, ts)
+    proc.punctuate(0)
+    blob = stores[P.NFA_STATES_STORE][("StockEvents", 0)]
+    assert blob[:8] == b"CEPPROC2"
+    n = int.from_bytes(blob[8:16], "little")
+    host = json.loads(blob[16 + n:].decode())
+    assert host["version"] == 2 and len(host["keys"]) == len(host["events"]) == len(host["base"])
+    proc2 = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
+    proc2.init(P.RecordContext("StockEvents", 0, stores=stores))
+    assert [[(e.offset, e.value) for e in evs] for evs in proc2._events] == \
+        [[(e.offset, e.value) for e in evs] for evs in proc._events]
+    with pytest.raises(ValueError):
+        proc2.restore(b"CEPPROC1" + blob[8:])
+
+    class Obj:
+        def __init__(self, name, price, volume):
+            self.name, self.price, self.volume = name, price, volume
+
+    proc3 = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
+    ctx3 = P.RecordContext("StockEvents", 0, stores={})
+    proc3.init(ctx3)
+    ctx3.send("k", Obj("e1", 100, 1010), 0)
+    with pytest.raises(TypeError):
+        proc3.punctuate(0)
