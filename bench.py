@@ -387,6 +387,41 @@ def streaming_cfg3(device, stream, slices, steps, dist, warmup=1, variant="readm
             "pairs_per_step": n_p, "key_errors": int(np.count_nonzero(code)), "checksum": f"{dig:016x}"}
 
 
+def processor_throughput(device, n_keys=10_000, per_key=100, batch=65_536):
+    """The reference's own entry point: CEPProcessor.process(key, value) (CEPProcessor.java:
+    155-163) called once per record, as a Kafka stream task calls it, on the README query, for
+    `n_keys` keys x `per_key` records of the cfg-3 generator interleaved round-robin (arrival
+    order), then close() (the flush).  processor.py buffers `batch` records per GPU push (a
+    streaming session's arrival-order batch) and forwards every Sequence in the reference's
+    order.  records/s = records / wall time of the process() calls + close(), host work
+    included: the Python host path, not the kernel, bounds this figure."""
+    from kafkastreams_cep_amd import processor as P
+    cfg = W.SynthConfig("proc", "stock", n_keys, per_key, W.CONFIGS[3].seed)
+    off, (price, vol) = W.generate(cfg)
+    off = off.astype(np.int64)
+    lens = np.diff(off)
+    order = []  # round-robin arrival: record r of every key before record r + 1 of any
+    for r in range(int(lens.max())):
+        ks = np.flatnonzero(lens > r)
+        order.append(off[ks] + r)
+    pos = np.concatenate(order)
+    kid = np.searchsorted(off, pos, side="right") - 1
+    recs = [(f"K{int(k)}", {"name": f"K{int(k)}", "price": int(price[p]), "volume": int(vol[p])}, int(i))
+            for i, (k, p) in enumerate(zip(kid, pos))]
+    ctx = P.RecordContext("StockEvents", 0)
+    proc = P.CEPProcessor(W.stock_query("readme"), in_memory=True, batch_size=batch, max_keys=n_keys, device=device)
+    proc.init(ctx)
+    t0 = time.perf_counter()
+    for k, v, ts in recs:
+        ctx.send(k, v, ts)
+    proc.close()
+    el = time.perf_counter() - t0
+    return {"workload": f"CEPProcessor.process() per record, README query, {n_keys} keys x {per_key} records "
+                        f"(round-robin arrival), batch {batch}, in_memory", "value": len(recs) / el,
+            "unit": "records/s", "records": len(recs), "forwarded": len(ctx.forwarded),
+            "matches_per_s": len(ctx.forwarded) / el, "seconds": el}
+
+
 def projected_scaling(device, cfg, stream, world, steps, dist, t1_ms=None):
     """SURVEY §8(e) strong scaling, projected on ONE GPU: every rank's murmur2 shard of the
     cfg-3 stream (shard.py, the same split bench.py makes at --gpus N) is run alone, one after
@@ -667,6 +702,9 @@ def main():
         if one and not args.no_streaming:
             log("streaming")
             out["streaming"] = streaming_cfg3(device, stream, 10, max(1, min(args.steps, 5)), dist)
+        if one and not args.no_streaming:
+            log("processor")
+            out["processor"] = processor_throughput(device)
         if one and not args.no_other:
             log("cfg4")
             # (a config-4 step is 5-10 ms: 10 timed steps after 3 warmup ones, the first of

@@ -276,7 +276,7 @@ typedef struct {
   uint64_t retried_jobs;   /* (query, key) jobs re-run */
   uint64_t nodes_used, preds_used, out_chunks_used;  /* buffer pools at the end of the batch */
   uint32_t launches;
-  uint32_t heavy_first;    /* group launches: queries run first by the heavy-first job order (0: none) */
+  uint32_t heavy_first;    /* reserved (0): the heavy-first job order was measured slower and removed */
 } cep_batch_stats;
 int cep_last_stats(cep_session* s, int query, cep_batch_stats* out);
 

@@ -64,7 +64,6 @@ struct Tuning {
   uint32_t walk_flush = 24;     // $CEP_WALK_FLUSH: the kernels' drain threshold (compile.cpp
                                 // compiles the same value in)
   uint32_t job_map = 0;         // $CEP_JOB_MAP (nfa_lane.h job_id)
-  bool heavy_first = false;     // $CEP_HEAVY_FIRST: the heavy-first job order of groups
   bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
   bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
   bool stream_no_order = false; // $CEP_STREAM_NO_ORDER

@@ -558,7 +558,9 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // a single query's narrow build never runs persistent lanes (session.cpp: only kernel groups
   // and the re-runs, which take the wide build, do): its kernel holds run() alone, half the code
   if (!lits.param) o += "#ifndef CEP_PERSIST_LANES\n#define CEP_PERSIST_LANES 0\n#endif\n";
-  o += "#define CEP_WAVES_EU 3\n#endif\n";
+  // (3 waves per SIMD; 2 with the wave-cooperative record pages, whose capture and resolution
+  // spill ~240 VGPRs at 3: filled in below once kCoop is known)
+  o += "#define CEP_WAVES_EU @@NARROW_WAVES@@\n#endif\n";
   // the wide build (6-pair Dewey versions: streams, re-runs) at 2 waves per SIMD: at 3 it
   // spills ~200 B of scratch and ran 20-25 % slower (profiles/r03)
   o += "#ifndef CEP_WAVES_EU\n#define CEP_WAVES_EU 2\n#endif\n";
@@ -676,23 +678,31 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       uint32_t sks = 0;
       bool ok = true;
     };
+    // (stage, edge) -> its predicate; a skip_till_next stage's IGNORE is NOT(edge 0's predicate)
+    // (StatesFactory.java:93-96): it never matches together with the consuming edge
+    std::vector<std::vector<const M*>> em(d.n_stages, std::vector<const M*>(3, nullptr));
+    for (auto& pe : b.pending) em[pe.stage][pe.edge] = pe.m.get();
     std::function<Bnd(int)> bnd = [&](int si) -> Bnd {
       const DevStage& S = d.st[si];
       Bnd r;
       if (S.type == ST_FINAL) return r;
-      bool hT = false, hB = false, hI = false;
+      bool hT = false, hB = false, hI = false, ignNot = false;
       int proc = -1;
       for (int e = 0; e < S.n_edges; e++) {
         if (S.e[e].op == OP_TAKE) hT = true;
         if (S.e[e].op == OP_BEGIN) hB = true;
-        if (S.e[e].op == OP_IGNORE) hI = true;
+        if (S.e[e].op == OP_IGNORE) {
+          hI = true;
+          const M* m = em[si][e];
+          ignNot = m && m->k == M::NOT && m->a.get() == em[si][0];
+        }
         if (S.e[e].op == OP_PROCEED) proc = (int)S.e[e].target;
       }
       Bnd t;
       if (proc >= 0 && proc != si) t = bnd(proc);
       if (proc == si) t.ok = false;  // (never built: a stage's PROCEED goes to its successor)
       const bool hP = proc >= 0, cons = hT || hB;
-      const bool canBr = (hP && hT) || (hI && hT) || (hI && hB) || (hI && hP);
+      const bool canBr = (hP && hT) || (hI && hT && !ignNot) || (hI && hB && !ignNot) || (hI && hP);
       r.p = (cons ? 1 : 0) + t.p;
       const int nb = std::max((cons || hI) ? 1 : 0, t.o);
       const int br = canBr ? (hB ? 1 : 0) + t.o + 1 : 0;
@@ -713,12 +723,25 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       all.sks |= b.sks;
       all.ok = all.ok && b.ok;
     }
+    // Opt-in ($CEP_COOP=1 at query compile): measured slower than the per-lane loop on config 3
+    // (43.1 vs 28.7 ms; the capture and the resolution need 2 waves per SIMD, 3 spill), and no
+    // faster on a lone heavy key (5.45 vs 5.49 ms: its per-event cost is not its record loop),
+    // DESIGN.md §10.1.  The CPU lane tests run the pages on whole emulated waves either way
+    // (tests/lane_cpu sets CEP_COOP_TESTS).
+    const bool want = std::getenv("CEP_COOP") != nullptr;
     const bool coop = quiet && !lits.param && all.ok && !((all.sks >> bs.sk) & 1u) && all.p <= 4 && all.o <= 4 &&
                       all.w <= 4;
-    o += "  static constexpr bool kCoop = " + std::string(coop ? "true" : "false") + ";  // nfa_coop.h\n";
+    o += std::string("#ifndef CEP_COOP_TESTS\n#define CEP_COOP_TESTS 0\n#endif\n");
+    // (the wide build - 6-pair versions: re-runs, streams - keeps the per-lane loop: its capture
+    // spills ~230 VGPRs at 2 waves per SIMD)
+    o += "  static constexpr bool kCoop = " +
+         std::string(coop ? (want ? "kDeweyPairs <= 3 || CEP_COOP_TESTS" : "CEP_COOP_TESTS") : "false") +
+         ";  // nfa_coop.h\n";
     o += "  static constexpr int kCoopP = " + std::to_string(std::max(all.p, 1)) + ", kCoopO = " +
          std::to_string(std::max(all.o, 1)) + ", kCoopW = " + std::to_string(std::max(all.w, 1)) + ";\n";
     o += "  static constexpr uint32_t kCoopSkMask = " + std::to_string(coop ? all.sks : 0u) + "u;\n";
+    const size_t at = o.find("@@NARROW_WAVES@@");
+    if (at != std::string::npos) o.replace(at, 16, coop && want ? "2" : "3");
   }
   o += "  typedef Ev EvT;\n";
   // another lane's event fields (coop pages step other lanes' records)

@@ -40,6 +40,7 @@
 // capture (kCoopP/O/W).  Otherwise, and for kernel groups, the per-lane loop runs.
 #pragma once
 
+
 namespace cep {
 
 constexpr uint32_t kTok = 0xFFFFFFF0u;  // a put's node as returned to the step: kTok | put slot

@@ -1255,7 +1255,9 @@ struct Lane {
 #pragma unroll
         for (int k = 0; k < X_t::kP; k++)
           if ((uint32_t)k < X.np && X.p_prev[k] != CEP_NONE) {
-            A.nodes[X.p_prev[k]].lk = opc_o + wbefore;
+            // (two records of the key may stamp one node in the same page: the later record's
+            // stamp, the larger, is the one the sequential order leaves)
+            atomicMax(&A.nodes[X.p_prev[k]].lk, opc_o + wbefore);
 #if CEP_PUT_LOG
             if (sslot >= A.plog) conflict = true;
             else *(PL(sslot) + d) = v4u{X.p_prev[k], opc_o + wbefore, j_o, 0u};
@@ -1487,6 +1489,19 @@ struct Lane {
     return jj < jn;
   }
 
+  // tick() with the records of the wave's events stepped together (nfa_coop.h).  Convergent:
+  // every lane of the wave, `more` false for a lane whose events are over.
+  __device__ __forceinline__ bool coop_tick(bool more) {
+    bool known = false;
+    const int st = more ? tick_pre(known) : 0;
+    const bool act = st == 2;
+    if (act) event_pre();
+    coop_records(act);
+    if (!act) return st == 1;
+    if (!err) event_post(known);
+    return tick_post();
+  }
+
   __device__ __forceinline__ bool tick() {
     bool known = false;
     const int st = tick_pre(known);
@@ -1532,21 +1547,13 @@ struct Lane {
       CEP_PT(tf1);
       CEP_PACC(0, tf1 - tf0);
       if constexpr (Q::kCoop) {
-        if (coop) {  // the records of the wave's events stepped together (nfa_coop.h)
-          bool known = false;
-          const int st = more ? tick_pre(known) : 0;
-          const bool act = st == 2;
-          if (act) event_pre();
-          coop_records(act);
-          if (act) {
-            if (!err) event_post(known);
-            more = tick_post();
-          } else {
-            more = st == 1;
-          }
-        } else if (more) {
-          more = tick();
-        }
+#if CEP_PERSIST_LANES
+        if (coop) more = coop_tick(more);
+        else if (more) more = tick();
+#else
+        // (a single query's narrow build: its only launch defers its walks, always coop)
+        more = coop_tick(more);
+#endif
       } else if (more) {
         more = tick();
       }

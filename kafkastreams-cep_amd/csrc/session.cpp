@@ -180,6 +180,7 @@ struct GroupRt {
   hipFunction_t fn = nullptr;
   hipModule_t mod_wide = nullptr;  // its wide build (compile.cpp generate_jit): re-runs, streams
   hipFunction_t fn_wide = nullptr;
+  uint32_t waves_cu = 0, waves_cu_wide = 0;  // resident waves per CU of fn / fn_wide (occupancy)
   hipFunction_t fn_est = nullptr;   // cep_nfa_est (begin stage = one BEGIN edge)
   hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
   double jit_compile_s = 0;
@@ -192,11 +193,6 @@ struct GroupRt {
   // pool use of the last batch (the next batch's pools are sized from it)
   uint64_t last_nodes = 0, last_preds = 0, last_out = 0;
   uint32_t rcap_hint = 0;  // run-queue slots per key: grown when a batch's queues overflowed
-  // work history for the heavy-first job order: emitted event ids per key of each member query
-  // in the last batch (empty before the first), and the query map of the order (NfaArgs.qmap)
-  std::vector<double> qwork;
-  std::vector<uint32_t> qmap_h;
-  DBuf qmap;
   cep_batch_stats stats{};  // the last batch
   ~GroupRt() {
     if (mod) (void)hipModuleUnload(mod);
@@ -299,10 +295,8 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint64_t nk = s->n_keys;
   const uint64_t n_tiles = stencil_tiles(s->n_events);
   const uint64_t n_groups = n_tiles / 64 + 2;
-  // counters, then group counts, group completions, the start ticket and the tile counts: one
-  // region, zeroed by the key-index pass before the stencil launch
-  const uint64_t n_zero = (sizeof(Scratch) + sizeof(uint32_t) * (2 * n_groups + 1 + n_tiles + 1)) / 4 + 1;
-  s->status.ensure(4 * n_zero);
+  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));                          // tile counts
+  s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
   s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
   s->bnd.ensure(sizeof(uint32_t) * (s->n_events / 64 + 2));                       // word -> key
@@ -349,10 +343,8 @@ void run_stencil(cep_session* s, QueryRt& r) {
   }
   for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
+  a.tile_cnt = s->tile_key.as<uint32_t>();
   a.group_cnt = reinterpret_cast<uint32_t*>(sc + 1);
-  a.group_done = a.group_cnt + n_groups;
-  a.ticket = a.group_done + n_groups;
-  a.tile_cnt = a.ticket + 1;
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
   a.total = &sc->total;
@@ -364,12 +356,12 @@ void run_stencil(cep_session* s, QueryRt& r) {
   // (4 % of this 0.12 ms step), so the 4 us key-index pass is not timed (aux_ms 0).
   // wave_keys also zeroes the counters (no memset launch); no D2H copy of them either
   HIPCHECK(launch_wave_keys(s->key_off, nk, s->n_events, s->keylist.as<uint32_t>(), reinterpret_cast<uint32_t*>(sc),
-                            (uint32_t)n_zero, s->stream));
+                            (uint32_t)((sizeof(Scratch) + sizeof(uint32_t) * n_groups) / 4), s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][1], s->stream));
   HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->tune.stencil_pf, s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][2], s->stream));
   r.pending = true;
-  r.launches = 1;  // stencil_fused (mask and emit roles)
+  r.launches = 2;  // stencil_mask + stencil_emit
   r.digest_valid = false;
   r.arity = m;
   // no per-key errors on this path: the predicates and folds are total
@@ -401,26 +393,6 @@ hipError_t launch_fn(hipFunction_t fn, NfaArgs& a, uint64_t blocks, hipStream_t 
 constexpr uint64_t kPoolMax = 0xFFFFFFF0ull;   // output chunk ids are u32
 constexpr uint64_t kNodeMax = 0x7FFFFFF0ull;   // node / pointer ids: 31 bits (kPred0 tags a node's slot)
 
-// The heavy queries of a group from its work history `w` (emitted ids per key of each member
-// in the last batch): those within 16x of the heaviest, when the heaviest is > 4x the median
-// and they are at most half the group.  qmap = the heavy ones, then the others (index order).
-static uint32_t heavy_queries(const std::vector<double>& w, std::vector<uint32_t>& qmap) {
-  const size_t Q = w.size();
-  if (Q < 2) return 0;
-  std::vector<double> srt(w);
-  std::sort(srt.begin(), srt.end());
-  const double mx = srt.back(), med = srt[Q / 2];
-  if (!(mx > 0) || mx <= 4 * med) return 0;
-  qmap.clear();
-  for (size_t q = 0; q < Q; q++)
-    if (w[q] * 16 >= mx) qmap.push_back((uint32_t)q);
-  const uint32_t nh = (uint32_t)qmap.size();
-  if (nh == 0 || nh > Q / 2) return 0;
-  for (size_t q = 0; q < Q; q++)
-    if (w[q] * 16 < mx) qmap.push_back((uint32_t)q);
-  return nh;
-}
-
 // Runs a kernel group over the batch: the begin-hit bitmap and lane order, the matching
 // launch, re-runs of the jobs that hit a capacity limit or a deferred-walk conflict, and the
 // per-query compaction of the output chains into flat arrays.
@@ -439,7 +411,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // lane per key (their run queues live at the key's slot).
   // waves per CU of the JIT kernels (compile.cpp): the narrow build 3 per SIMD, the wide one
   // (streams, re-runs) 2; $CEP_RESIDENT_WAVES (per CU): measurement runs
-  uint64_t waves_cu = streaming ? 8 : 12, waves_cu_wide = 8;
+  const uint64_t wn = g.waves_cu ? g.waves_cu : 12, ww = g.waves_cu_wide ? g.waves_cu_wide : 8;
+  uint64_t waves_cu = streaming ? ww : wn, waves_cu_wide = ww;
   if (s->tune.resident_waves > 0) waves_cu = waves_cu_wide = s->tune.resident_waves;
   const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
   const uint64_t resident_wide = (uint64_t)s->cus * waves_cu_wide * 64;
@@ -581,19 +554,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
     a.job_map = s->tune.job_map;  // (measurement runs)
-    // Heavy-first ($CEP_HEAVY_FIRST, opt-in): when the last batch's output was concentrated in
-    // a few queries (config 5: the 8 variants with the loosest dip predicate emit ~95 % of the
-    // event ids), their jobs go first.  Measured slower on config 5 (4.55 / 3.94 s against
-    // 3.81 / 2.95 s per batch, profiles/r03_cfg5_ab.sh): waves of heavy jobs only drain worse
-    // than the key-major waves, whose light lanes keep claiming jobs beside the heavy ones.
-    // Results do not depend on the order.
-    const uint32_t nh = heavy_queries(g.qwork, g.qmap_h);
-    if (nh > 0 && s->tune.heavy_first) {
-      g.qmap.ensure(4 * Q);
-      HIPCHECK(hipMemcpyAsync(g.qmap.p, g.qmap_h.data(), 4 * Q, hipMemcpyHostToDevice, s->stream));
-      a.qmap = g.qmap.as<uint32_t>();
-      a.n_heavy = nh;
-    }
   }
   if (streaming) {  // walks deferred too: a conflict resolves exactly without a re-run (nfa_lane.h)
     a.rings = S.rings.p;
@@ -694,7 +654,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // re-run too).
   // The job lists are collected on the device; only their lengths come back.
   g.stats = cep_batch_stats{};
-  g.stats.heavy_first = a.qmap ? a.n_heavy : 0;
   g.stats.group_queries = (uint32_t)Q;
   float main_ms = 0;
   HIPCHECK(hipEventElapsedTime(&main_ms, s->ev2, s->ev1));
@@ -795,8 +754,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
     HIPCHECK(hipStreamSynchronize(s->stream));
     r.n_matches = tot[0];
     r.n_pairs = tot[1];
-    if (g.qwork.size() != Q) g.qwork.assign(Q, 0.0);
-    g.qwork[qi] = nk ? (double)(tot[0] + tot[1]) / (double)nk : 0.0;
     r.m_key.ensure(sizeof(uint32_t) * (tot[0] + 1));
     r.m_emit.ensure(sizeof(uint32_t) * (tot[0] + 1));
     r.m_off.ensure(sizeof(uint64_t) * (tot[0] + 1));
@@ -1006,6 +963,14 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         g->jit_compile_s += w;
         HIPCHECK(hipModuleLoadData(&g->mod_wide, cw.data()));
         HIPCHECK(hipModuleGetFunction(&g->fn_wide, g->mod_wide, "cep_nfa_jit"));
+        // the kernels' occupancy (waves per SIMD as compiled: 3 narrow, 2 wide or coop) sizes the
+        // persistent and spread grids (run_nfa)
+        int nb = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, g->fn, 256, 0) == hipSuccess && nb > 0)
+          g->waves_cu = (uint32_t)nb * 4;
+        nb = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, g->fn_wide, 256, 0) == hipSuccess && nb > 0)
+          g->waves_cu_wide = (uint32_t)nb * 4;
         if (pl.source.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
           HIPCHECK(hipModuleGetFunction(&g->fn_est, g->mod, "cep_nfa_est"));
           HIPCHECK(hipModuleGetFunction(&g->fn_bits, g->mod, "cep_nfa_bits"));

@@ -14,21 +14,14 @@
 // from a bitmap built once per batch, so a window crossing a key start is masked with
 // shifts, and a match's key is the tile's first key advanced by the key starts before it.
 //
-// One launch, two roles (stencil_fused).  A block takes a ticket when it starts (an atomic
-// counter, so tickets follow the order blocks actually run in); tickets 0..T-1 are the mask
-// role of tile t = ticket, T..2T-1 the emit role of tile t = ticket - T.  (1) The mask role
-// streams its 16384 events once (a wave issues all its loads before the first is used),
-// writes one 64-bit match mask per 64 events (1 bit/event) and publishes the tile's count
-// (tile_cnt, and per 64 tiles group_cnt / group_done).  (2) The emit role waits until its tile
-// and every tile before it have published (a wait only on lower tickets, which are running or
-// done: no deadlock whatever the residency), sums the counts before its tile, reads the masks
-// back (1/32 of the column's bytes) and writes the matches in order.  The emit roles run in
-// the slots the mask roles free, overlapping the tail of the streaming instead of a second
-// launch after it (a whole-batch look-back inside the streaming pass was measured
-// latency-bound here: rounds of co-resident tiles look back through each other).
+// Passes.  (1) stencil_mask streams the column once (a wave issues all its loads before the
+// first is used) and writes one 64-bit match mask per 64 events (1 bit/event) and a count per
+// tile; (2) stencil_emit sums the counts of the tiles before its own, reads the masks back
+// (1/32 of the column's bytes) and writes the matches in order.  No tile waits on another, so the streaming pass runs at HBM rate (a single-pass
+// decoupled look-back was measured latency-bound here: rounds of co-resident tiles look back
+// through each other).
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <type_traits>
 
 #include "cep_layout.h"
@@ -179,20 +172,15 @@ struct StEval {
   }
 };
 
-// acquire load at agent scope (another CU's release store of the value is visible, and the
-// loads after it see what that CU wrote before it)
-__device__ __forceinline__ uint32_t ld_acquire(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int M, bool RANGE, int NCOL, int PF>
-__device__ __forceinline__ void mask_tile(const StencilArgs& A, uint64_t tile, uint32_t* s_cnt) {
+__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   static_assert(kStSteps % PF == 0, "prefetch depth divides the wave's steps");
   constexpr int H = M - 1;              // events a window reaches back
+  __shared__ uint32_t s_cnt[kStThreads / 64];
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
   // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t wbase = tile * kStTile + (uint64_t)wv * kStWave;
+  const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
   const StEval<M, RANGE, NCOL> ev(A);
   const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never;
   // The fast path's first PF steps are requested before anything else: the key-start words
@@ -401,15 +389,11 @@ __device__ __forceinline__ void mask_tile(const StencilArgs& A, uint64_t tile, u
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if (lane == 0) s_cnt[wv] = cnt;
-  __threadfence();  // this thread's mask / key words reach L2 before the tile is published
   __syncthreads();
   if (threadIdx.x == 0) {
-    // publish: the group's count first, then the tile (count + 1: nonzero = published) and the
-    // group's completion, both release stores
     const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-    if (c) atomicAdd(A.group_cnt + tile / kStGroup, c);
-    __hip_atomic_store(A.tile_cnt + tile, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(A.group_done + tile / kStGroup, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    A.tile_cnt[blockIdx.x] = c;
+    if (c) atomicAdd(A.group_cnt + blockIdx.x / kStGroup, c);  // per 64 tiles, for stencil_emit
   }
 }
 
@@ -426,32 +410,15 @@ __device__ __forceinline__ uint64_t spread4(uint32_t x16) {
 // Pass 2: a thread per 64 events (a quarter of a step's ballot words), the tile's offset
 // from the group and tile counts, a block scan for the threads' offsets.  A match's key is
 // the thread's first key (word_key) advanced over the key offsets it passes.
-// a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
-constexpr uint32_t kStage = 2048;
-struct EmitLds {
-  uint32_t wsum[kStThreads / 64];
-  uint64_t toff[kStThreads / 64];
-  uint2 stage[kStage];  // (key, sequence number of the final event)
-};
-
 template <int M>
-__device__ __forceinline__ void emit_tile(const StencilArgs& A, uint64_t t, uint64_t n_tiles, EmitLds& L) {
-  uint32_t* s_wsum = L.wsum;
-  uint64_t* s_toff = L.toff;
-  uint2* s_stage = L.stage;
+__global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
+  // a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
+  constexpr uint32_t kStage = 2048;
+  __shared__ uint32_t s_wsum[kStThreads / 64];
+  __shared__ uint64_t s_toff[kStThreads / 64];
+  __shared__ uint2 s_stage[kStage];  // (key, sequence number of the final event)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  {
-    // wait until this tile and every tile before it are published (mask roles hold lower
-    // tickets: they run or ran, and wait on nothing)
-    const uint64_t g = t / kStGroup, g0 = g * kStGroup;
-    for (uint64_t i = tid; i < g; i += kStThreads)
-      while (ld_acquire(A.group_done + i) < kStGroup) __builtin_amdgcn_s_sleep(2);
-    if (tid <= t - g0)
-      while (ld_acquire(A.tile_cnt + g0 + tid) == 0) __builtin_amdgcn_s_sleep(2);
-    // (the L1 may hold lines of the counts or masks from before they were final: drop them)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-  }
+  const uint64_t t = blockIdx.x;
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
   // Every independent load is issued before the first use (addresses clamped, no branches):
   // the step (256 events) holding this thread's 64 - 16 lanes of each of its 4 ballot words -
@@ -486,8 +453,8 @@ __device__ __forceinline__ void emit_tile(const StencilArgs& A, uint64_t t, uint
   // group before it (cheaper than a scan launch between the passes)
   uint64_t part = 0;
   const uint64_t g0 = (t / kStGroup) * kStGroup;
-  for (uint64_t i = tid; i < t / kStGroup; i += kStThreads) part += ld_acquire(A.group_cnt + i);
-  if (g0 + tid < t) part += ld_acquire(A.tile_cnt + g0 + tid) - 1;  // (published as count + 1)
+  for (uint64_t i = tid; i < t / kStGroup; i += kStThreads) part += A.group_cnt[i];
+  if (g0 + tid < t) part += A.tile_cnt[g0 + tid];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
   if (lane == 63) s_wsum[wv] = incl;
@@ -499,7 +466,7 @@ __device__ __forceinline__ void emit_tile(const StencilArgs& A, uint64_t t, uint
     if (w < wv) woff += s_wsum[w];
   const uint32_t excl = woff + incl - cnt;
   const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
-  if (t + 1 == n_tiles && tid == kStThreads - 1) {  // all matches
+  if (t + 1 == gridDim.x && tid == kStThreads - 1) {  // all matches
     *A.total = toff + woff + incl;
     if (A.total_host) *A.total_host = toff + woff + incl;  // pinned host memory, read after the batch's event
   }
@@ -550,19 +517,6 @@ __device__ __forceinline__ void emit_tile(const StencilArgs& A, uint64_t t, uint
   }
 }
 
-// The one launch: 2T blocks, roles by start ticket (header)
-template <int M, bool RANGE, int NCOL, int PF>
-__global__ void __launch_bounds__(kStThreads) stencil_fused(StencilArgs A) {
-  __shared__ uint32_t s_ticket;
-  __shared__ uint32_t s_cnt[kStThreads / 64];
-  __shared__ EmitLds s_emit;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(A.ticket, 1u);
-  __syncthreads();
-  const uint64_t k = s_ticket, n_tiles = gridDim.x / 2;
-  if (k < n_tiles) mask_tile<M, RANGE, NCOL, PF>(A, k, s_cnt);
-  else emit_tile<M>(A, k - n_tiles, n_tiles, s_emit);
-}
-
 // ---------------------------------------------------------------- host launchers
 hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
                             uint32_t* zero, uint32_t n_zero, hipStream_t st) {
@@ -577,14 +531,15 @@ uint64_t stencil_waves(uint64_t n_events) { return (n_events + kStWave - 1) / kS
 
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, int pf0, hipStream_t st) {
-  const dim3 g((uint32_t)(2 * n_tiles)), b(kStThreads);
-  // prefetch depth of the mask role's fast path (steps of 256 events whose loads run ahead;
+  const dim3 g((uint32_t)n_tiles), b(kStThreads);
+  // prefetch depth of stencil_mask's fast path (steps of 256 events whose loads run ahead;
   // the session's $CEP_STENCIL_PF knob, else kStDefaultPF); only the range fast path streams
   // vector loads
   const int pf = RANGE ? (pf0 == 1 || pf0 == 2 || pf0 == 4 ? pf0 : kStDefaultPF) : 1;
-  if (pf == 4) hipLaunchKernelGGL((stencil_fused<M, RANGE, NCOL, RANGE ? 4 : 1>), g, b, 0, st, a);
-  else if (pf == 2) hipLaunchKernelGGL((stencil_fused<M, RANGE, NCOL, RANGE ? 2 : 1>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((stencil_fused<M, RANGE, NCOL, 1>), g, b, 0, st, a);
+  if (pf == 4) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 4 : 1>), g, b, 0, st, a);
+  else if (pf == 2) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 2 : 1>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, 1>), g, b, 0, st, a);
+  hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -26,10 +26,8 @@ struct StencilArgs {
   // pass 1 -> pass 3
   uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k
   uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1)
-  uint32_t* tile_cnt;        // matches per tile + 1, 0 until the mask role published it (zeroed per batch)
-  uint32_t* group_cnt;       // matches per 64 tiles (mask roles, atomics; zeroed per batch)
-  uint32_t* group_done;      // tiles of each group of 64 published (zeroed per batch)
-  uint32_t* ticket;          // start tickets of the fused launch (zeroed per batch)
+  uint32_t* tile_cnt;        // matches per tile (pass 1)
+  uint32_t* group_cnt;       // matches per 64 tiles (pass 1, atomics; zeroed per batch)
   // output
   uint32_t* m_key;
   uint32_t* p_seq;           // [n_matches * m]

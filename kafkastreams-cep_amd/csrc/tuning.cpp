@@ -34,7 +34,6 @@ Tuning tuning_from_env() {
   t.walk_cap = wc > 0 ? (uint32_t)wc : 0u;
   t.walk_flush = tuning_walk_flush();
   t.job_map = (uint32_t)num("CEP_JOB_MAP", 0);
-  t.heavy_first = flag("CEP_HEAVY_FIRST");
   t.prof = flag("CEP_PROF");
   t.stream_narrow = flag("CEP_STREAM_NARROW");
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");

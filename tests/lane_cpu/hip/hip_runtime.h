@@ -53,6 +53,11 @@ inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v)
   if (v > o) *p = v;
   return o;
 }
+inline unsigned atomicMax(unsigned* p, unsigned v) {
+  const unsigned o = *p;
+  if (v > o) *p = v;
+  return o;
+}
 inline unsigned atomicOr(unsigned* p, unsigned v) {
   const unsigned o = *p;
   *p = o | v;
@@ -61,6 +66,7 @@ inline unsigned atomicOr(unsigned* p, unsigned v) {
 inline void __syncthreads() {}  // (the NFA kernels do not synchronise their waves)
 // a wave of one lane (no emulated wave): the coop pages (nfa_coop.h) need a whole wave
 #define CEP_HOST_LANES 1
+#define CEP_COOP_TESTS 1  // (compile.cpp: the coop pages on every qualifying query and build)
 inline bool cep_host_single_lane() { return emu::g_wave == nullptr; }
 
 #define CEP_EMU_SITE __FILE__ ":" CEP_EMU_STR(__LINE__)

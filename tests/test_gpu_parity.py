@@ -193,7 +193,6 @@ def test_cfg5_medium_bit_exact():
     qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)]
     s = N.Session(qs)
     s.push(off, cols)
-    assert s.stats(0)["heavy_first"] == 0  # (no work history yet)
     total, want = 0, []
     for i, q in enumerate(qs):
         r = oracle.run(q.ir, off, cols, threads=16)
@@ -201,17 +200,7 @@ def test_cfg5_medium_bit_exact():
         want.append(r)
         assert_parity(session_result(s, i, off), r, off)
     assert total > 50000
-    # the second batch with the heavy-first job order (opt-in: the 8 dip-95 variants' jobs first)
-    os.environ["CEP_HEAVY_FIRST"] = "1"
-    try:
-        s.push(off, cols)
-    finally:
-        del os.environ["CEP_HEAVY_FIRST"]
-    assert s.stats(0)["heavy_first"] > 0
-    for i, r in enumerate(want):
-        assert_parity(session_result(s, i, off), r, off)
-    s.push(off, cols)  # (the default order again)
-    assert s.stats(0)["heavy_first"] == 0
+    s.push(off, cols)  # a second batch of the same session (pools sized from the first)
     for i, r in enumerate(want):
         assert_parity(session_result(s, i, off), r, off)
 

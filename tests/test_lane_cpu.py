@@ -179,18 +179,6 @@ def test_lane_query_group():
         lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
 
 
-def test_lane_query_group_heavy_first(monkeypatch):
-    """The heavy-first job order of a group launch (NfaArgs.qmap: the heavy queries' jobs over
-    every key first, then the others'), with a heavy part whose size does not divide 64."""
-    monkeypatch.setenv("CEP_LANE_QMAP", "3")
-    cfg = W.SynthConfig("t", "stock", 70, 300, 0xCE90000 + 6)
-    off, cols = W.generate(cfg)
-    irs = [p.to_ir() for p in W.multi_queries(64)[48:64]]
-    res = lane_cpu.run_group(irs, off, cols)
-    for ir, g in zip(irs, res):
-        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
-
-
 @pytest.mark.parametrize("seed", list(range(0, 160, 16)) + [21, 80, 393, 571])
 def test_lane_partial_drains(seed, monkeypatch):
     """Partial drains (nfa_lane.h flush(may_stop)) forced at every flush, with a 4-walk flush
