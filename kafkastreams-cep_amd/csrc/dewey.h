@@ -59,6 +59,16 @@ __device__ __forceinline__ void dw_init(Dewey& d, int32_t v) {
   }
 }
 
+// the same version (canonical encodings: the same pairs in use)
+__device__ __forceinline__ bool dw_equal(const Dewey& a0, const Dewey& b0) {
+  const Dewey a = dw_pin(a0), b = dw_pin(b0);
+  bool eq = a.n == b.n;
+#pragma unroll
+  for (int k = 0; k < P; k++)
+    if ((uint32_t)k < a.n) eq = eq && a.v[k] == b.v[k] && a.c[k] == b.c[k];
+  return eq;
+}
+
 __device__ __forceinline__ int32_t dw_last(const Dewey& d0) {
   const Dewey d = dw_pin(d0);
   int32_t r = d.v[0];

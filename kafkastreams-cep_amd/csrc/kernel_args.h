@@ -45,11 +45,6 @@ struct NfaArgs {
   uint32_t spread_snake;     // spread: odd lanes take their row of ranks in reverse
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
-  // heavy-first order (group launches with a work history, session.cpp): the jobs of the
-  // n_heavy queries qmap[0, n_heavy) on every key first, then those of the others qmap[n_heavy,
-  // n_q), each part query-minor over the ranks; null = the mapping above
-  const uint32_t* qmap;
-  uint32_t n_heavy;
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
   Node* nodes;
   Pred* preds;               // the predecessor pool (a node's second and later pointers)

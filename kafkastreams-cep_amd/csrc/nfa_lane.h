@@ -81,7 +81,7 @@
 
 // Work counters for the CPU lane build (tests/lane_cpu, CEP_LANE_STATS); nothing on the GPU.
 #ifdef CEP_LANE_STATS
-extern uint64_t cep_lane_stats[9];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters, exact conflicts
+extern uint64_t cep_lane_stats[10];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters, exact conflicts, twin writes saved
 #define CEP_STAT(i) (cep_lane_stats[i]++)
 #else
 #define CEP_STAT(i) ((void)0)
@@ -177,6 +177,20 @@ typedef CEP_LDS_AS v4u lds_v4u;
 #include "nfa_coop.h"
 namespace cep {
 
+// Twin slots.  A record that a step re-adds unchanged (an IGNORE without a new stage: the
+// reference re-adds the same object, NFA.java:225) at the slot it was read from already sits,
+// word for word, in the other queue half if it sat there two events ago: header bit kTwin of a
+// stored record says "the other half's copy of this slot is the same record", kTwinT says "and
+// that copy's kTwin is set".  The record's write is then reduced to its header (kTwin) or
+// dropped (kTwin and kTwinT).  Only HBM slots (the LDS slots are cheap to write) - config 4's
+// ~20 runs a key holds were read and rewritten every event (54x its algorithmic
+// bytes).  A copy's flags are read only when the copy is an event's input, and an event's
+// input half was its previous event's output half, whose every slot in use was written or
+// kept with the guarantee; anything that changes a record in place (clear_hints, the finals'
+// compaction) clears them.
+constexpr uint32_t kTwin = 1u << 23, kTwinT = 1u << 22;
+constexpr uint32_t kStageMask = 0x003FFFFFu;  // the stage word bits of a stored header's x
+
 // W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
 template <int F, bool W32 = false>
 struct RecLayout {
@@ -241,6 +255,11 @@ struct Lane {
   uint32_t ncur = 0, nend = 0, pcur = 0, pend = 0;
   uint32_t ochunk = CEP_NONE, opos = 0;
   uint32_t ocur = 0, oend = 0;  // output chunks in hand (kept across the jobs of a persistent lane)
+  // twin slots: the record being stepped (its slot, its stored head quad) and a re-add of it
+  // whose head write waits for its folds
+  uint32_t in_slot = CEP_NONE, pend_slot = CEP_NONE;
+  v4u in_raw = {0, 0, 0, 0};
+  const Rec<F>* in_rec = nullptr;
   uint32_t cur_first = CEP_NONE;  // node chain of event j
   uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending; coop pages)
   // chain cache (kCC > 0): packed stage keys (byte k) | count << 24 (> kCC: overflow/invalid)
@@ -322,9 +341,10 @@ struct Lane {
   // ---------------------------------------------------------------- records
   // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
   __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf, int d = 0,
-                                       v4u* b = nullptr) const {
+                                       v4u* b = nullptr, v4u* raw = nullptr) const {
     const v4u hd = rd(h, slot, 0, d, b);
-    r.stage = hd.x & 0x00FFFFFFu;
+    if (raw) *raw = hd;
+    r.stage = hd.x & kStageMask;
     r.event = hd.y;
     r.ev_first = hd.z == kPending ? pf : hd.z;
     r.node = hd.w;
@@ -362,9 +382,9 @@ struct Lane {
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
                                              uint32_t ev_first, const Dewey& ver0, uint32_t node, int d = 0,
-                                             v4u* b = nullptr) {
+                                             v4u* b = nullptr, uint32_t flags = 0) {
     const Dewey ver = dw_pin(ver0);
-    wr(h, slot, 0, v4u{stage | (ver.n << 24), event, ev_first, node}, d, b);
+    wr(h, slot, 0, v4u{stage | flags | (ver.n << 24), event, ev_first, node}, d, b);
 #pragma unroll
     for (int k = 0; k < Lay::kDwQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
@@ -393,9 +413,14 @@ struct Lane {
       wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]}, d, b);
   }
 
+  // (a record moved to another slot: its twin flags do not hold there)
   __device__ __forceinline__ void copy_rec(uint32_t h, uint32_t from, uint32_t to) {
 #pragma unroll
-    for (int k = 0; k < Lay::kQuads; k++) wr(h, to, k, rd(h, from, k));
+    for (int k = 0; k < Lay::kQuads; k++) {
+      v4u q4 = rd(h, from, k);
+      if (k == 0) q4.x &= ~(kTwin | kTwinT);
+      wr(h, to, k, q4);
+    }
   }
 
   // Appends an output record (header + version) and returns its slot, -1 when the queue is
@@ -410,12 +435,40 @@ struct Lane {
     }
     const uint32_t slot = ocount++;
     const uint32_t ef = (event == j && ev_first == CEP_NONE) ? kPending : ev_first;
-    store_head(half ^ 1u, slot, stage, event, ef, ver, node);
     if (stage & kRecFinal) n_final++;
+    // the record stepped, re-added unchanged so far at its own slot (twin slots): its head is
+    // written with its folds, once they are known equal or not (set_folds)
+    if (slot == in_slot && slot >= kRL && stage == (in_raw.x & kStageMask) && event == in_raw.y && ef == in_raw.z &&
+        node == in_raw.w && dw_equal(ver, in_rec->ver)) {
+      pend_slot = slot;
+      return (int)slot;
+    }
+    store_head(half ^ 1u, slot, stage, event, ef, ver, node);
     return (int)slot;
   }
 
   __device__ __forceinline__ void set_folds(int slot, const int64_t* v, uint32_t nm) {
+    if ((uint32_t)slot == pend_slot) {  // the head equals the input record's (push_rec)
+      pend_slot = CEP_NONE;
+      bool same = nm == in_rec->nullmask;
+#pragma unroll
+      for (int k = 0; k < F; k++) same = same && v[k] == in_rec->fold[k];
+      const uint32_t st = in_raw.x & kStageMask;
+      if (same) {
+        if ((in_raw.x & kTwin) && (in_raw.x & kTwinT)) {  // the other half holds it, flags set
+          CEP_STAT(9);
+          return;
+        }
+        if (in_raw.x & kTwin) {  // the other half holds it: its header, with the flags
+          CEP_STAT(9);
+          wr(half ^ 1u, (uint32_t)slot, 0, v4u{st | kTwin | kTwinT | (in_raw.x & 0xFF000000u), in_raw.y, in_raw.z, in_raw.w});
+          return;
+        }
+        store_head(half ^ 1u, (uint32_t)slot, st, in_raw.y, in_raw.z, in_rec->ver, in_raw.w, 0, nullptr, kTwin);
+      } else {
+        store_head(half ^ 1u, (uint32_t)slot, st, in_raw.y, in_raw.z, in_rec->ver, in_raw.w);
+      }
+    }
     store_folds(half ^ 1u, (uint32_t)slot, v, nm);
   }
 
@@ -585,6 +638,7 @@ struct Lane {
       v4u hd = rd(half, i, 0);
       if (hd.w != CEP_NONE) {
         hd.w = CEP_NONE;
+        hd.x &= ~(kTwin | kTwinT);  // (changed in place: no longer its twin's copy)
         wr(half, i, 0, hd);
       }
     }
@@ -1091,8 +1145,11 @@ struct Lane {
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
       CEP_STAT(1);
-      load(half, i, c, pf_ev);
+      load(half, i, c, pf_ev, 0, nullptr, &in_raw);
+      in_slot = i;
+      in_rec = &c;
       const int produced = q.step(*this, c);
+      in_slot = CEP_NONE;
       if (err) return;
       CEP_PACC(9, 1);
       if (produced == 0) {  // removePattern
@@ -1415,7 +1472,7 @@ struct Lane {
   __device__ __forceinline__ bool only_begin() const {
     if (kBeginReg) return count == 0;
     if (count != 1) return false;
-    return (rd(half, 0, 0).x & 0x00FFFFFFu) == q.begin_stage;
+    return (rd(half, 0, 0).x & kStageMask) == q.begin_stage;
   }
 
   // ---------------------------------------------------------------- the job's event loop
@@ -1629,14 +1686,6 @@ struct Lane {
 __device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
   if (A.jobs) return A.jobs[idx];
   const uint32_t nq = A.n_q ? A.n_q : 1;
-  if (A.qmap) {  // heavy-first: the heavy queries' jobs over all ranks, then the light ones'
-    const uint64_t nh = (uint64_t)A.n_heavy * A.n_keys;
-    const uint64_t i = idx < nh ? idx : idx - nh;
-    const uint32_t np = idx < nh ? A.n_heavy : nq - A.n_heavy;
-    const uint64_t rank = i / np;
-    const uint32_t qi = A.qmap[(idx < nh ? 0u : A.n_heavy) + (uint32_t)(i % np)];
-    return (uint64_t)qi * A.n_keys + (A.order ? A.order[rank] : rank);
-  }
   uint64_t rank = idx / nq;
   uint32_t qi = (uint32_t)(idx % nq);
   if (A.job_map == 1 && nq % 8 == 0) {

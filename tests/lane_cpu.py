@@ -96,10 +96,10 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bit
     m = {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
          "pair_seq": seq, "pair_stage": stage, "err_code": err, "err_seq": err_seq,
          "retried": retried.value, "bits_used": bool(lib.lane_bits_used())}
-    st = (C.c_uint64 * 9)()
+    st = (C.c_uint64 * 10)()
     lib.lane_stats(st)
     m["stats"] = dict(zip(("events", "records", "walks", "walk_nodes", "pred_scans", "flushes", "chain_steps",
-                           "flush_iters", "exact_conflicts"), list(st)))
+                           "flush_iters", "exact_conflicts", "twin_writes_saved"), list(st)))
     if _group:
         return m
     m["emit_pos"] = (key_off[key.astype(np.int64)] + emit).astype(np.uint64)

@@ -17,7 +17,7 @@
 thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
 
 static void wave_body(void* a) { cep_nfa_jit(*static_cast<cep::NfaArgs*>(a)); }
-uint64_t cep_lane_stats[9];
+uint64_t cep_lane_stats[10];
 extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
 
 namespace {
@@ -127,17 +127,6 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   a.n_capacity_err = &n_cap;
   a.n_q = n_q;
   a.kc = kc;
-  // $CEP_LANE_QMAP=h: the heavy-first job order (session.cpp) with the last h queries heavy
-  std::vector<uint32_t> qmap;
-  if (const char* e = std::getenv("CEP_LANE_QMAP")) {
-    const uint32_t h = (uint32_t)std::atoi(e);
-    if (h > 0 && h < n_q) {
-      for (uint32_t q = n_q - h; q < n_q; q++) qmap.push_back(q);
-      for (uint32_t q = 0; q < n_q - h; q++) qmap.push_back(q);
-      a.qmap = qmap.data();
-      a.n_heavy = h;
-    }
-  }
   a.n_events = ne;
   std::vector<uint64_t> bits((ne + 63) / 64 + 1, 0);
   g_bits_used = use_bits && fill_bits(a, bits, 0);
