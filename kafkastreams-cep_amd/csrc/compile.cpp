@@ -869,7 +869,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
       f += "          if (L.err) return;\n";
       f += "          sw = " + consWord + ";\n          e0 = L.j;\n          ef = CEP_NONE;\n          consumed = true;\n        }\n";
     }
-    f += "        const int r = L.push_rec(sw, e0, ef, ver, nd);\n";
+    f += "        const int r = L.push_rec(sw, e0, ef, ver, nd, !consumed);  // (!consumed: the record re-added as it is)\n";
     f += "        if (r < 0) return;\n        o.same = r;\n        o.produced++;\n      }\n";
     f += "    } else {\n";
     // branching: every matched edge in edge order, then the branch record

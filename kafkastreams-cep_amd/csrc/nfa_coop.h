@@ -132,7 +132,7 @@ struct RecCtx {
   }
 
   __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver,
-                                          uint32_t node = CEP_NONE) {
+                                          uint32_t node = CEP_NONE, bool = false) {
     if (no >= (uint32_t)kO) {
       err = KE_RETRY;
       return -1;

@@ -189,6 +189,7 @@ namespace cep {
 // kept with the guarantee; anything that changes a record in place (clear_hints, the finals'
 // compaction) clears them.
 constexpr uint32_t kTwin = 1u << 23, kTwinT = 1u << 22;
+constexpr uint32_t kInPend = 1u << 16;  // (Lane::in_info only)
 constexpr uint32_t kStageMask = 0x003FFFFFu;  // the stage word bits of a stored header's x
 
 // W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
@@ -257,9 +258,9 @@ struct Lane {
   uint32_t ocur = 0, oend = 0;  // output chunks in hand (kept across the jobs of a persistent lane)
   // twin slots: the record being stepped (its slot, its stored head quad) and a re-add of it
   // whose head write waits for its folds
-  uint32_t in_slot = CEP_NONE, pend_slot = CEP_NONE;
-  v4u in_raw = {0, 0, 0, 0};
-  const Rec<F>* in_rec = nullptr;
+  // in_info: its Dewey length (bits 0-15; a longer one never matches) | its stored twin flags |
+  // kInPend (stored ev_first kPending)
+  uint32_t in_slot = CEP_NONE, pend_slot = CEP_NONE, in_info = 0;
   uint32_t cur_first = CEP_NONE;  // node chain of event j
   uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending; coop pages)
   // chain cache (kCC > 0): packed stage keys (byte k) | count << 24 (> kCC: overflow/invalid)
@@ -426,8 +427,12 @@ struct Lane {
   // Appends an output record (header + version) and returns its slot, -1 when the queue is
   // full.  ev_first of a record whose event is the current one is only known once the
   // event's nodes exist: kPending, resolved at its next load.  Folds: set_folds.
+  // `keep`: a non-consuming re-add of the record being stepped (IGNORE, NFA.java:225): its folds
+  // are the record's own, and with its own version (the same Dewey length: on this path the
+  // version is the record's with zero or more addStage digits) and head it is the same record -
+  // at its own HBM slot, the twin slots spare its rewrite (header above).
   __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver,
-                                          uint32_t node = CEP_NONE) {
+                                          uint32_t node = CEP_NONE, bool keep = false) {
     if (ocount >= A.rcap) {
       err = KE_RETRY;
       if (A.full) atomicOr(A.full, 1u);
@@ -436,11 +441,19 @@ struct Lane {
     const uint32_t slot = ocount++;
     const uint32_t ef = (event == j && ev_first == CEP_NONE) ? kPending : ev_first;
     if (stage & kRecFinal) n_final++;
-    // the record stepped, re-added unchanged so far at its own slot (twin slots): its head is
-    // written with its folds, once they are known equal or not (set_folds)
-    if (slot == in_slot && slot >= kRL && stage == (in_raw.x & kStageMask) && event == in_raw.y && ef == in_raw.z &&
-        node == in_raw.w && dw_equal(ver, in_rec->ver)) {
+    // (on the keep path the stage word, event and node hint are the record's own - sw is its
+    // stage word with its own branching flag - so the head differs from the stored one only
+    // when the stored ev_first was kPending: in_info bit kInPend)
+    if (keep && slot == in_slot && slot >= kRL && (in_info & kInPend) == 0 && ver.len == (in_info & 0xFFFFu)) {
+      if (!(in_info & kTwin)) {  // the output copy is stale: written whole, marked the input's twin
+        store_head(half ^ 1u, slot, stage, event, ef, ver, node, 0, nullptr, kTwin);
+        return (int)slot;
+      }
+      // the output copy already holds it: at most its header's flags, never its folds
+      CEP_STAT(9);
       pend_slot = slot;
+      if (!(in_info & kTwinT))
+        wr(half ^ 1u, slot, 0, v4u{stage | kTwin | kTwinT | (ver.n << 24), event, ef, node});
       return (int)slot;
     }
     store_head(half ^ 1u, slot, stage, event, ef, ver, node);
@@ -448,26 +461,9 @@ struct Lane {
   }
 
   __device__ __forceinline__ void set_folds(int slot, const int64_t* v, uint32_t nm) {
-    if ((uint32_t)slot == pend_slot) {  // the head equals the input record's (push_rec)
+    if ((uint32_t)slot == pend_slot) {  // a kept twin: its folds are in place (push_rec)
       pend_slot = CEP_NONE;
-      bool same = nm == in_rec->nullmask;
-#pragma unroll
-      for (int k = 0; k < F; k++) same = same && v[k] == in_rec->fold[k];
-      const uint32_t st = in_raw.x & kStageMask;
-      if (same) {
-        if ((in_raw.x & kTwin) && (in_raw.x & kTwinT)) {  // the other half holds it, flags set
-          CEP_STAT(9);
-          return;
-        }
-        if (in_raw.x & kTwin) {  // the other half holds it: its header, with the flags
-          CEP_STAT(9);
-          wr(half ^ 1u, (uint32_t)slot, 0, v4u{st | kTwin | kTwinT | (in_raw.x & 0xFF000000u), in_raw.y, in_raw.z, in_raw.w});
-          return;
-        }
-        store_head(half ^ 1u, (uint32_t)slot, st, in_raw.y, in_raw.z, in_rec->ver, in_raw.w, 0, nullptr, kTwin);
-      } else {
-        store_head(half ^ 1u, (uint32_t)slot, st, in_raw.y, in_raw.z, in_rec->ver, in_raw.w);
-      }
+      return;
     }
     store_folds(half ^ 1u, (uint32_t)slot, v, nm);
   }
@@ -1145,9 +1141,10 @@ struct Lane {
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
       CEP_STAT(1);
-      load(half, i, c, pf_ev, 0, nullptr, &in_raw);
+      v4u raw;
+      load(half, i, c, pf_ev, 0, nullptr, &raw);
       in_slot = i;
-      in_rec = &c;
+      in_info = (c.ver.len & 0xFFFFu) | (raw.x & (kTwin | kTwinT)) | (raw.z == kPending ? kInPend : 0u);
       const int produced = q.step(*this, c);
       in_slot = CEP_NONE;
       if (err) return;
