@@ -299,7 +299,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
   s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
-  s->bnd.ensure(sizeof(uint32_t) * (s->n_events / 64 + 2));                       // word -> key
+  s->bnd.ensure(sizeof(uint32_t) * 2 * (s->n_events / 64 + 2));                   // word -> key, sequence number
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
   if (!r.h_sc) HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocMapped));
@@ -327,6 +327,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   a.key_off = s->key_off;
   a.wave_key = s->keylist.as<uint32_t>();
   a.word_key = s->bnd.as<uint32_t>();
+  a.word_seq = a.word_key + (s->n_events / 64 + 2);
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.cols = s->cols;

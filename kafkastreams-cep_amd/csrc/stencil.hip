@@ -221,11 +221,15 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   const uint64_t ws = wbase + (uint64_t)lane * 64;
   uint64_t bw = 0;
   uint32_t pkb = 0, wkey = k0;
+  uint64_t wks = 0;  // wkey's first event (stencil_emit: sequence numbers without key_off)
   if (wbase < A.n_events) {
     for (int64_t i0 = (int64_t)k0 - 8;; i0 += 64) {
       const int64_t i = i0 + lane;
       const bool valid = i >= 0 && (uint64_t)i < A.n_keys;
       const uint64_t sj = valid ? A.key_off[i] : 0;
+      if (i0 == (int64_t)k0 - 8)  // (lane 8 of the first chunk read k0's offset)
+        wks = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sj >> 32), 8) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, 8);
       uint64_t inr = __ballot(valid && sj >= lo && sj < wend);
       while (inr) {
         const int j = __builtin_ctzll(inr);
@@ -237,7 +241,10 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
         } else {
           pkb |= 1u << (uint32_t)(sjj - (wbase - 8));
         }
-        if (sjj <= ws) wkey = (uint32_t)(i0 + j);
+        if (sjj <= ws) {
+          wkey = (uint32_t)(i0 + j);
+          wks = sjj;
+        }
       }
       const uint64_t s63 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sj >> 32), 63) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, 63);
@@ -383,7 +390,12 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   }
   // one 512-B store: words 4q..4q+3 belong to step q (written when the step has an event)
   if (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) A.mask[wbase / 64 + lane] = myword;
-  if (ws < A.n_events) A.word_key[wbase / 64 + lane] = wkey;
+  // (bit 31: a key starts inside the word after its first event - stencil_emit walks key_off
+  // there; elsewhere a match's sequence number is word_seq + its offset in the word)
+  if (ws < A.n_events) {
+    A.word_key[wbase / 64 + lane] = wkey | ((bw & ~1ull) ? 0x80000000u : 0u);
+    A.word_seq[wbase / 64 + lane] = (uint32_t)(ws - wks);
+  }
   // matches of the wave: popcount of each lane's word, summed over the wave once
   uint32_t cnt = (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) ? (uint32_t)__popcll(myword) : 0u;
 #pragma unroll
@@ -427,7 +439,9 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const uint64_t pc = valid ? p0 : t * kStTile;  // a tile's first event always exists
   const uint64_t* w = A.mask + (pc / 256) * 4;
   const uint64_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-  uint32_t key = A.word_key[pc / 64];
+  const uint32_t wk = A.word_key[pc / 64], seq0 = A.word_seq[pc / 64];
+  uint32_t key = wk & 0x7FFFFFFFu;
+  const bool cross = (wk >> 31) != 0;  // a key starts inside this thread's 64 events
   uint32_t ck[4] = {0, 0, 0, 0};
   if (valid) {
     const int sh = 16 * (int)((p0 / 64) & 3);
@@ -438,7 +452,7 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   }
   const uint32_t cnt = __popc(ck[0]) + __popc(ck[1]) + __popc(ck[2]) + __popc(ck[3]);
   uint64_t kstart = 0, knext = 0;
-  if (cnt) {
+  if (cnt && cross) {
     kstart = A.key_off[key];
     knext = A.key_off[key + 1];
   }
@@ -480,12 +494,15 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
     const int i = __builtin_ctzll(match);
     match &= match - 1;
     const uint64_t p = p0 + i;
-    while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
-      key++;
-      kstart = knext;
-      knext = A.key_off[key + 1];
+    uint32_t seq = seq0 + (uint32_t)i;
+    if (cross) {
+      while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
+        key++;
+        kstart = knext;
+        knext = A.key_off[key + 1];
+      }
+      seq = (uint32_t)(p - kstart);
     }
-    const uint32_t seq = (uint32_t)(p - kstart);
     if (staged) {
       s_stage[so++] = uint2{key, seq};
     } else if (o < A.out_cap) {

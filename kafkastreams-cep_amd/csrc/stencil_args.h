@@ -25,7 +25,9 @@ struct StencilArgs {
   bool aligned;              // col[] 16-B aligned: vector loads
   // pass 1 -> pass 3
   uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k
-  uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1)
+  uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1); bit 31: a key
+                             // starts inside the word after its first event
+  uint32_t* word_seq;        // event 64 w's sequence number within that key (pass 1)
   uint32_t* tile_cnt;        // matches per tile (pass 1)
   uint32_t* group_cnt;       // matches per 64 tiles (pass 1, atomics; zeroed per batch)
   // output
