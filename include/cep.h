@@ -272,8 +272,10 @@ typedef struct {
   uint32_t group_queries;  /* queries in that launch */
   double kernel_ms;        /* bitmap + lane order + matching launch + re-runs */
   double main_ms;          /* the matching launch (cep_nfa_jit / nfa_kernel) alone */
-  double retry_ms;         /* re-runs of jobs that hit a capacity limit or a walk conflict */
-  uint64_t retried_jobs;   /* (query, key) jobs re-run */
+  double retry_ms;         /* re-runs of jobs that hit a capacity limit or a walk conflict
+                              (streams: the wide build's continuation of stopped keys) */
+  uint64_t retried_jobs;   /* (query, key) jobs re-run (streams: keys whose versions outgrew
+                              the stream build's 3 pairs, continued by the wide build) */
   uint64_t nodes_used, preds_used, out_chunks_used;  /* buffer pools at the end of the batch */
   uint32_t launches;
   uint32_t heavy_first;    /* reserved (0): the heavy-first job order was measured slower and removed */

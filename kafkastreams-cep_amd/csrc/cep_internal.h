@@ -58,6 +58,7 @@ struct Tuning {
   uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
   bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too
   int spread = 2;               // $CEP_SPREAD: 0 off, 1 rows in order, 2 odd lanes reversed
+  uint32_t isolate = 0;         // $CEP_ISOLATE: heaviest ranks of a spread launch alone in their waves
   uint32_t node_chunk = 0;      // $CEP_NODE_CHUNK: pool range per lane (0: default)
   uint32_t out_chunk = 0;       // $CEP_OUT_CHUNK
   uint32_t walk_cap = 0;        // $CEP_WALK_CAP: deferred walks per lane (0: default)
@@ -66,6 +67,7 @@ struct Tuning {
   uint32_t job_map = 0;         // $CEP_JOB_MAP (nfa_lane.h job_id)
   bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
   bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
+  bool stream_wide = false;     // $CEP_STREAM_WIDE: streams on the wide build even when the stream build holds
   bool stream_no_order = false; // $CEP_STREAM_NO_ORDER
   bool no_wm_fold = false;      // $CEP_NO_WM_FOLD: the watermark as its own pass
   int stencil_pf = 0;           // $CEP_STENCIL_PF: 1, 2 or 4 (0: default)
@@ -113,6 +115,15 @@ std::vector<char> jit_code_object(const std::string& src, double* compile_s);
 // the wide build of a generated kernel (6 Dewey pairs; the source as generated is the narrow
 // build): capacity re-runs and streaming sessions run it
 inline std::string jit_wide_source(const std::string& src) { return "#define CEP_DEWEY_PAIRS 6\n" + src; }
+// the stream build (streaming sessions): 3-pair versions in registers at the narrow build's 3
+// waves per SIMD, in the wide build's memory layout (a stream's records and pointers outlive the
+// launch); the put log (a stream cannot re-run a key: walk conflicts resolved in place); a key
+// whose versions outgrow 3 pairs stops before that event for the wide build to continue
+// (CEP_STREAM_STOP, nfa_lane.h stop_event)
+inline std::string jit_stream_source(const std::string& src) {
+  return "#define CEP_DEWEY_PAIRS 3\n#define CEP_LAYOUT_PAIRS 6\n#define CEP_PUT_LOG 1\n#define CEP_STREAM_STOP 1\n"
+         "#define CEP_PERSIST_LANES 0\n#define CEP_WAVES_EU 3\n" + src;
+}
 struct Cols;
 size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,

@@ -26,6 +26,14 @@ constexpr int kMaxStack = 16;      // interpreter stack depth
 #define CEP_DEWEY_PAIRS 6
 #endif
 constexpr int kDeweyPairs = CEP_DEWEY_PAIRS;
+// Pairs the memory layout has room for (run records, predecessor pointers, walk queue
+// entries): a stream's state outlives a launch, so the stream build (3 pairs in registers,
+// session.cpp) keeps the wide build's layout and a key it stops continues in the wide build.
+#ifndef CEP_LAYOUT_PAIRS
+#define CEP_LAYOUT_PAIRS CEP_DEWEY_PAIRS
+#endif
+constexpr int kLayoutPairs = CEP_LAYOUT_PAIRS;
+static_assert(kLayoutPairs >= kDeweyPairs, "the layout holds every pair in registers");
 constexpr int kMaxStencil = 8;     // stages of a CEP_KIND_STENCIL query (stencil.hip instantiations)
 
 enum StateType : uint8_t { ST_BEGIN = 0, ST_NORMAL = 1, ST_FINAL = 2 };
@@ -34,9 +42,12 @@ enum EdgeOp : uint8_t { OP_BEGIN = 0, OP_TAKE = 1, OP_PROCEED = 2, OP_IGNORE = 3
 // walks than the queue holds (nfa_lane.h); internal, the key is re-run with walks in place.  KE_RETRY: a resource of the launch ran out (run
 // queue, walk queue, node / predecessor / output pool); internal, the key is re-run with more.
 // KE_CAPACITY: a hard limit (Dewey RLE pairs, stage depth): final.  A KE_RETRY left after the
-// last re-run is reported as KE_CAPACITY.
+// last re-run is reported as KE_CAPACITY.  KE_WIDEN (streams, internal): the stream build's
+// versions outgrew 3 pairs at an event; the key stopped before it and the wide build continues it
+// (nfa_lane.h stop_event, session.cpp run_nfa).
 enum KeyErr : int32_t {
-  KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16, KE_CONFLICT = 17, KE_RETRY = 18
+  KE_OK = 0, KE_NPE = 1, KE_ILLEGAL_STATE = 2, KE_ARITH = 3, KE_CAPACITY = 16, KE_CONFLICT = 17, KE_RETRY = 18,
+  KE_WIDEN = 19
 };
 
 constexpr uint16_t kProgTrue = 0xFFFF;
@@ -117,7 +128,7 @@ struct alignas(16) Pred {
   uint32_t next;   // next Pred of the node, CEP_NONE = end
   uint32_t flags;  // bit0 removed, [15:8] Dewey pairs in use
   uint32_t len;
-  uint32_t pair[2 * kDeweyPairs];  // v0, c0, v1, c1, ...
+  uint32_t pair[2 * kLayoutPairs];  // v0, c0, v1, c1, ...
 };
 
 // ---- per-key NFA state carried from one batch to the next (streaming sessions): what the
@@ -133,7 +144,8 @@ struct KeyCarry {
   uint32_t opc;        // walks queued so far (deferred-walk ids)
   int32_t err;         // sticky: the exception that stopped the key
   uint32_t err_seq;
-  uint32_t pad[3];
+  uint32_t bseq;       // KE_WIDEN: sequence number of the batch's first event of the key
+  uint32_t pad[2];
 };
 
 // ---- per-key state kept between kernel phases
@@ -143,7 +155,8 @@ struct KeyState {
   uint32_t out_first;  // first output chunk (CEP_NONE: no output)
   int32_t err;
   uint32_t err_seq;
-  uint32_t pad[3];
+  uint32_t ochunk, opos;  // KE_WIDEN: where the key's output continues
+  uint32_t pad;
 };
 
 constexpr uint32_t kOutChunkWords = 256;  // output stream chunk (last word links the next)

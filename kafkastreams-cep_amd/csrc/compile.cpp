@@ -735,7 +735,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     // (the wide build - 6-pair versions: re-runs, streams - keeps the per-lane loop: its capture
     // spills ~230 VGPRs at 2 waves per SIMD)
     o += "  static constexpr bool kCoop = " +
-         std::string(coop ? (want ? "kDeweyPairs <= 3 || CEP_COOP_TESTS" : "CEP_COOP_TESTS") : "false") +
+         std::string(coop ? (want ? "(kDeweyPairs <= 3 || CEP_COOP_TESTS) && !CEP_STREAM_STOP" : "CEP_COOP_TESTS && !CEP_STREAM_STOP") : "false") +
          ";  // nfa_coop.h\n";
     o += "  static constexpr int kCoopP = " + std::to_string(std::max(all.p, 1)) + ", kCoopO = " +
          std::to_string(std::max(all.o, 1)) + ", kCoopW = " + std::to_string(std::max(all.w, 1)) + ";\n";

@@ -43,6 +43,8 @@ struct NfaArgs {
   uint64_t spread;           // W > 0: an underfilled single-query launch of W waves, wave w's lane l
                              // running rank l * W + w (session.cpp run_nfa); 0: rank w * 64 + l
   uint32_t spread_snake;     // spread: odd lanes take their row of ranks in reverse
+  uint32_t spread_iso;       // spread: the K = spread_iso heaviest ranks run alone, one per wave (waves
+                             // 0..K-1, lane 0); the other ranks spread over waves K..W-1
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
@@ -53,6 +55,8 @@ struct NfaArgs {
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;
   KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
+  uint32_t widen;            // streaming: this launch continues the listed jobs the stream build
+                             // stopped (KE_WIDEN) from their carried event, output appended
   uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)
   uint64_t* bhits;           // cep_nfa_bits: bit p = the begin predicate (null folds) is true or
                              // throws at CSR position p (quiet lanes jump to the next set bit)

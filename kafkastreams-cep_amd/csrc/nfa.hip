@@ -412,14 +412,15 @@ __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint6
 }
 
 // jobs to re-run: KE_RETRY -> cap_list, KE_CONFLICT -> conf_list (any order: jobs are
-// independent); counts[0..1] their lengths
+// independent); counts[0..1] their lengths.  (Streams: KE_WIDEN -> conf_list, the keys to
+// continue; a stream never reports KE_CONFLICT)
 __global__ void __launch_bounds__(256) collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_list,
                                                      uint32_t* conf_list, uint32_t* counts) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int e = ks[i].err;
   if (e == KE_RETRY) cap_list[atomicAdd(counts, 1u)] = (uint32_t)i;
-  else if (e == KE_CONFLICT) conf_list[atomicAdd(counts + 1, 1u)] = (uint32_t)i;
+  else if (e == KE_CONFLICT || e == KE_WIDEN) conf_list[atomicAdd(counts + 1, 1u)] = (uint32_t)i;
 }
 
 // One wave per heavy key: the chain is read a whole 1 KiB chunk per wave load (each lane 16 B =

@@ -130,7 +130,7 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
 constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
-constexpr int kWalkQuads = 2 + (kDeweyPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
+constexpr int kWalkQuads = 2 + (kLayoutPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
 // the entry's `first` field holds the walk's start node itself (the record's node hint, live
 // when the walk was queued - an epsilon record's hint is its node of (stage key, event)): no
@@ -151,7 +151,10 @@ constexpr uint32_t kWalkHint = 8;
 #endif
 // a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
 // re-runs the job in the wide one (a retry); the wide build's limit is final
-constexpr int32_t kDwFull = kDeweyPairs < 6 ? KE_RETRY : KE_CAPACITY;
+#ifndef CEP_STREAM_STOP
+#define CEP_STREAM_STOP 0
+#endif
+constexpr int32_t kDwFull = kDeweyPairs >= 6 ? KE_CAPACITY : CEP_STREAM_STOP ? KE_WIDEN : KE_RETRY;
 // Node-chain cache (deferred walks only): the nodes this lane made at the current event and
 // at the previous one, up to kCC each, kept in registers so that put()'s predecessor lookup
 // and the current event's node lookup need no memory round trip.  Exact: every node of an
@@ -195,7 +198,8 @@ constexpr uint32_t kStageMask = 0x003FFFFFu;  // the stage word bits of a stored
 // W32: every fold state is a 32-bit int (one word per slot, the query's own choice)
 template <int F, bool W32 = false>
 struct RecLayout {
-  static constexpr int kDwQuads = (kDeweyPairs + 1) / 2;
+  static constexpr int kDwQuads = (kLayoutPairs + 1) / 2;  // (memory)
+  static constexpr int kDwRegQuads = (kDeweyPairs + 1) / 2;  // the quads a version in registers fills
   static constexpr int kFoldQuads = W32 ? (1 + F + 3) / 4 : (2 + 2 * F + 3) / 4;
   static constexpr int kQuads = 1 + kDwQuads + kFoldQuads;
   // quads of an LDS slot: header, Dewey quad 0, folds
@@ -219,7 +223,7 @@ __host__ __device__ constexpr int ring_lds_slots() {
 // bytes of double-buffered run queues for n_slots lanes of rcap records (64-bit folds: the
 // larger layout, so one allocation serves every query)
 __host__ __device__ inline uint64_t ring_bytes(int F, uint64_t n_slots, uint32_t rcap) {
-  const int quads = 1 + (kDeweyPairs + 1) / 2 + (2 + 2 * F + 3) / 4;
+  const int quads = 1 + (kLayoutPairs + 1) / 2 + (2 + 2 * F + 3) / 4;
   return ((n_slots + 63) / 64) * 64ull * 2ull * rcap * quads * 16ull;
 }
 
@@ -276,6 +280,7 @@ struct Lane {
   uint32_t opc = 0;   // walks queued since the key started (walk ids)
   uint32_t pl_n = 0;  // put-log entries since the last flush
   uint32_t wt_last = CEP_NONE, wm0 = 0, wp0 = 0;  // event of the last walk run, counts before it
+  uint32_t stop_j = CEP_NONE;  // CEP_STREAM_STOP: the event the key stopped before (KE_WIDEN)
 #ifdef CEP_PROF
   unsigned long long prof[14] = {};  // the time split (see CEP_PROF above), this wave / lane
   // lane 0 adds the wave's cycles, the lane counters summed over the wave
@@ -351,7 +356,7 @@ struct Lane {
     r.node = hd.w;
     r.ver.n = hd.x >> 24;
 #pragma unroll
-    for (int k = 0; k < Lay::kDwQuads; k++) {
+    for (int k = 0; k < Lay::kDwRegQuads; k++) {
       v4u dq = {0, 0, 0, 0};
       if ((uint32_t)(2 * k) < r.ver.n) dq = rd(h, slot, 1 + k, d, b);
       r.ver.v[2 * k] = (int32_t)dq.x;
@@ -387,7 +392,7 @@ struct Lane {
     const Dewey ver = dw_pin(ver0);
     wr(h, slot, 0, v4u{stage | flags | (ver.n << 24), event, ev_first, node}, d, b);
 #pragma unroll
-    for (int k = 0; k < Lay::kDwQuads; k++)
+    for (int k = 0; k < Lay::kDwRegQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
         wr(h, slot, 1 + k, v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
                                2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
@@ -433,6 +438,14 @@ struct Lane {
   // at its own HBM slot, the twin slots spare its rewrite (header above).
   __device__ __forceinline__ int push_rec(uint32_t stage, uint32_t event, uint32_t ev_first, const Dewey& ver,
                                           uint32_t node = CEP_NONE, bool keep = false) {
+#if CEP_STREAM_STOP && defined(CEP_TEST_WIDEN)
+    // (tests/lane_cpu: stops at pseudo-random records mid-event, after earlier records' puts,
+    // pushes and walks, so the undo and the continuation are exercised on every query)
+    if (A.carry && ev_pos == j && ((j * 2654435761u) ^ (key * 40503u) ^ (ocount * 97u)) % CEP_TEST_WIDEN == 0) {
+      err = KE_WIDEN;
+      return -1;
+    }
+#endif
     if (ocount >= A.rcap) {
       err = KE_RETRY;
       if (A.full) atomicOr(A.full, 1u);
@@ -1560,9 +1573,54 @@ struct Lane {
     bool known = false;
     const int st = tick_pre(known);
     if (st != 2) return st == 1;
+#if CEP_STREAM_STOP
+    const uint32_t wq0 = wq_n;
     event(known);
+    if (err == KE_WIDEN) {
+      stop_event(wq0);
+      return false;
+    }
+#else
+    event(known);
+#endif
     return tick_post();
   }
+
+#if CEP_STREAM_STOP
+  // The stream build's versions outgrew 3 pairs at event j (kDwFull): the key stops BEFORE j, as
+  // the previous event left it, and the wide build continues it from j (run_key, session.cpp).
+  // What event j did so far is undone - no walk runs inside an event, so it touched only:
+  //  - the walks it queued: dropped (ids reused: the continuation queues the same ones);
+  //  - the nodes of (_, j) it made or rewrote (its chain, cur_first): dead, unreachable from
+  //    any record or pointer of an older event; cur_first back to event j - 1's chain;
+  //  - records written to the other queue half: never read (half and count stay), but a twin
+  //    slot there (kTwin) may have been overwritten: the input records' twin flags are cleared;
+  //  - stamps and put-log entries of the puts that found a node live: kept.  The stop's drain
+  //    (run: the walks queued before j) then finds the conflicts the reference would throw at j
+  //    (IllegalState at a put of j that precedes the overflowing record), and a stamp left for
+  //    the continuation is the one its identical put writes again (same walks queued before it).
+  __device__ __forceinline__ void stop_event(uint32_t wq0) {
+    opc -= wq_n - wq0;
+    wq_n = wq0;
+    for (uint32_t i = cur_first; i != CEP_NONE;) {
+      v4u n1 = *NQ(i, 1);
+      const uint32_t nx = n1.x;
+      n1.y &= ~0x100u;
+      *NQ(i, 1) = n1;
+      i = nx;
+    }
+    cur_first = pf_ev;
+    for (uint32_t i = 0; i < count; i++) {
+      v4u hd = rd(half, i, 0);
+      if (hd.x & (kTwin | kTwinT)) {
+        hd.x &= ~(kTwin | kTwinT);
+        wr(half, i, 0, hd);
+      }
+    }
+    stop_j = j;
+    err = KE_OK;
+  }
+#endif
 
   // the step's exception, after the final drain found nothing earlier (drained: flush() ran)
   __device__ __forceinline__ void finish_err() {
@@ -1830,8 +1888,15 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     // ...; spread_snake: odd lanes take their row in reverse (wave 0's lane 1 is the row's
     // lightest key), so the waves of the heaviest keys carry the lightest neighbours
     const uint64_t l = slot % 64;
-    const uint64_t rank = A.spread ? l * A.spread + ((A.spread_snake && (l & 1)) ? A.spread - 1 - w : w)
-                                   : (w / nq) * 64 + l;
+    uint64_t rank;
+    if (A.spread && w < A.spread_iso) {  // a heavy rank alone in its wave: no divergent neighbours
+      rank = l == 0 ? w : ~0ull;
+    } else if (A.spread) {
+      const uint64_t W = A.spread - A.spread_iso, w2 = w - A.spread_iso;
+      rank = A.spread_iso + l * W + ((A.spread_snake && (l & 1)) ? W - 1 - w2 : w2);
+    } else {
+      rank = (w / nq) * 64 + l;
+    }
     if (rank >= A.n_keys) has = false;
     else job = (w % nq) * A.n_keys + (A.order ? A.order[rank] : rank);
   }
@@ -1861,8 +1926,19 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     kc = nullptr;
     L.n_ev = 0;
   }
-  if (kc && kc->live) {  // the key's NFA as the previous batch left it
+  uint32_t bseq = 0;  // sequence number of the batch's first event of the key
+  if (kc && kc->live) {  // the key's NFA as the previous batch (or this batch's stop) left it
     L.j0 = kc->seq;
+    bseq = L.j0;
+    if (A.widen) {  // continue a key the stream build stopped (KE_WIDEN) at its event kc->seq
+      bseq = kc->bseq;
+      L.n_ev -= L.j0 - bseq;
+      L.n_matches = ks.n_matches;
+      L.n_pairs = ks.n_pairs;
+      L.out_first = ks.out_first;
+      L.ochunk = ks.ochunk;
+      L.opos = ks.opos;
+    }
     L.half = kc->half;
     L.count = kc->count;
     L.bdig = kc->bdig;
@@ -1888,7 +1964,7 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
       L.count = 1;
     }
   }
-  L.base = has ? A.key_off[key] - L.j0 : 0;
+  L.base = has ? A.key_off[key] - bseq : 0;
   L.run();
   if (!has) return;
   ks.n_matches = L.n_matches;
@@ -1896,11 +1972,18 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   ks.out_first = L.out_first;
   ks.err = L.err;
   ks.err_seq = L.err_seq;
-  if (L.err == KE_RETRY || L.err == KE_CONFLICT) atomicAdd(A.n_capacity_err, 1u);
+  const bool stopped = L.stop_j != CEP_NONE && !L.err;  // (its drain threw: stopped for good)
+  if (stopped) {
+    ks.err = KE_WIDEN;
+    ks.ochunk = L.ochunk;
+    ks.opos = L.opos;
+  }
+  if (L.err == KE_RETRY || L.err == KE_CONFLICT || stopped) atomicAdd(A.n_capacity_err, 1u);
   if (kc) {
     if (!L.err) L.lds_spill(true);  // LDS ends with the launch: the queue continues from HBM
     kc->live = 1;
-    kc->seq = L.j0 + L.n_ev;
+    kc->seq = stopped ? L.stop_j : L.j0 + L.n_ev;
+    kc->bseq = bseq;
     kc->half = L.half;
     kc->count = L.count;
     kc->bdig = L.bdig;

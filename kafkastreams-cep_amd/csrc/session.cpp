@@ -180,6 +180,8 @@ struct GroupRt {
   hipFunction_t fn = nullptr;
   hipModule_t mod_wide = nullptr;  // its wide build (compile.cpp generate_jit): re-runs, streams
   hipFunction_t fn_wide = nullptr;
+  hipModule_t mod_stream = nullptr;  // streaming sessions: the stream build (jit_stream_source)
+  hipFunction_t fn_stream = nullptr;
   uint32_t waves_cu = 0, waves_cu_wide = 0;  // resident waves per CU of fn / fn_wide (occupancy)
   hipFunction_t fn_est = nullptr;   // cep_nfa_est (begin stage = one BEGIN edge)
   hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
@@ -193,10 +195,12 @@ struct GroupRt {
   // pool use of the last batch (the next batch's pools are sized from it)
   uint64_t last_nodes = 0, last_preds = 0, last_out = 0;
   uint32_t rcap_hint = 0;  // run-queue slots per key: grown when a batch's queues overflowed
+  uint64_t stream_widened = 0;  // keys the wide build continued (KE_WIDEN), over the session
   cep_batch_stats stats{};  // the last batch
   ~GroupRt() {
     if (mod) (void)hipModuleUnload(mod);
     if (mod_wide) (void)hipModuleUnload(mod_wide);
+    if (mod_stream) (void)hipModuleUnload(mod_stream);
     if (sort_tmp) (void)hipFree(sort_tmp);
   }
 };
@@ -438,6 +442,12 @@ void run_nfa(cep_session* s, GroupRt& g) {
     if (mode != 0) spread = std::min<uint64_t>(resident / 64, nk);
     snake = mode == 2 ? 1u : 0u;
   }
+  // heavy ranks alone in their waves (measurement knob): only while the rest still fit
+  uint32_t iso = 0;
+  if (spread && s->tune.isolate) {
+    iso = (uint32_t)std::min<uint64_t>(s->tune.isolate, spread - 1);
+    while (iso > 0 && (uint64_t)iso + (spread - iso) * 64 < nk) iso /= 2;
+  }
   const uint64_t slots = spread ? spread * 64 : !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
@@ -539,6 +549,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.n_q = (uint32_t)Q;
   a.spread = spread;
   a.spread_snake = snake;
+  a.spread_iso = iso;
   a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
   a.preds = s->preds.as<Pred>();
@@ -612,7 +623,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // error - and $CEP_STREAM_NO_ORDER: without the lane order; measurement runs only)
   const bool stream_narrow = s->tune.stream_narrow;
   if (streaming && s->tune.stream_no_order) a.order = nullptr;
-  HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
+  if (streaming && g.fn_stream) HIPCHECK(launch_fn(g.fn_stream, a, (slots + 255) / 256, s->stream));
+  else HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
   Scratch h{};
@@ -630,6 +642,42 @@ void run_nfa(cep_session* s, GroupRt& g) {
   float ms = 0;
   HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
   total_ms += ms;
+  float main_ms = 0;  // the matching launch alone (before any continuation below)
+  HIPCHECK(hipEventElapsedTime(&main_ms, s->ev2, s->ev1));
+  uint32_t widened = 0;  // keys the wide build continued (streams), and its launch time
+  float widen_ms = 0;
+  if (streaming && g.fn_stream && h.n_cap_err > 0) {
+    // keys the stream build stopped before an event their versions outgrew 3 pairs at
+    // (KE_WIDEN): the wide build continues each from that event over the same state
+    s->keylist.ensure(sizeof(uint32_t) * 2 * h.n_cap_err);
+    uint32_t* cap_list = s->keylist.as<uint32_t>();
+    uint32_t* widen_list = cap_list + h.n_cap_err;
+    HIPCHECK(hipMemsetAsync(&sc->n_retry_cap, 0, 2 * sizeof(uint32_t), s->stream));
+    HIPCHECK(launch_collect_retry(g.ks.as<KeyState>(), jobs, cap_list, widen_list, &sc->n_retry_cap, s->stream));
+    uint32_t lens[2];
+    HIPCHECK(hipMemcpyAsync(lens, &sc->n_retry_cap, sizeof lens, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    if (lens[1]) {
+      a.jobs = widen_list;
+      a.n_jobs = lens[1];
+      a.widen = 1;
+      a.order = nullptr;
+      a.spread = 0;
+      a.spread_iso = 0;
+      HIPCHECK(hipEventRecord(s->ev0, s->stream));
+      HIPCHECK(launch_nfa_tier(g, r0.q, a, lens[1], s->stream, true));
+      HIPCHECK(hipEventRecord(s->ev1, s->stream));
+      launches++;
+      HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipStreamSynchronize(s->stream));
+      HIPCHECK(hipEventElapsedTime(&widen_ms, s->ev0, s->ev1));
+      total_ms += widen_ms;
+      widened = lens[1];
+      g.stream_widened += lens[1];
+      a.jobs = nullptr;
+      a.widen = 0;
+    }
+  }
   if (streaming) {  // no re-runs: a key that hit a limit keeps its error (sticky, reported)
     uint32_t tops[2];
     HIPCHECK(hipMemcpy(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost));
@@ -656,9 +704,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // The job lists are collected on the device; only their lengths come back.
   g.stats = cep_batch_stats{};
   g.stats.group_queries = (uint32_t)Q;
-  float main_ms = 0;
-  HIPCHECK(hipEventElapsedTime(&main_ms, s->ev2, s->ev1));
   g.stats.main_ms = main_ms;
+  g.stats.retried_jobs = widened;  // (streams: the keys the wide build continued)
+  g.stats.retry_ms = widen_ms;
   for (int round = 0; h.n_cap_err > 0 && round < 8; round++) {
     const uint64_t nlist = h.n_cap_err;
     s->keylist.ensure(sizeof(uint32_t) * 2 * nlist);
@@ -709,6 +757,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     a.walks = s->walks.p;
     a.order = nullptr;
     a.spread = 0;
+    a.spread_iso = 0;
     HIPCHECK(hipEventRecord(s->ev0, s->stream));
     // capacity re-runs keep deferred walks; conflicts too (the wide build resolves them
     // exactly through its put log, nfa_lane.h), except after a put log overflowed: in place
@@ -831,6 +880,8 @@ int cep_jit_precompile(const cep_query* q, double* compile_s) {
     double w = 0;
     jit_code_object(q->jitSource, compile_s);
     jit_code_object(jit_wide_source(q->jitSource), &w);
+    if (compile_s) *compile_s += w;
+    jit_code_object(jit_stream_source(q->jitSource), &w);  // (streaming sessions over the query)
     if (compile_s) *compile_s += w;
   } catch (std::exception& e) {
     return fail(CEP_E_COMPILE, e.what());
@@ -964,6 +1015,14 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         g->jit_compile_s += w;
         HIPCHECK(hipModuleLoadData(&g->mod_wide, cw.data()));
         HIPCHECK(hipModuleGetFunction(&g->fn_wide, g->mod_wide, "cep_nfa_jit"));
+        // streams run the stream build: 3-pair versions at 3 waves per SIMD, a key whose
+        // versions outgrow them continued by the wide build (run_nfa)
+        if (s->opts.streaming && !s->tune.stream_wide && !s->tune.stream_narrow) {
+          std::vector<char> cs = jit_code_object(jit_stream_source(pl.source), &w);
+          g->jit_compile_s += w;
+          HIPCHECK(hipModuleLoadData(&g->mod_stream, cs.data()));
+          HIPCHECK(hipModuleGetFunction(&g->fn_stream, g->mod_stream, "cep_nfa_jit"));
+        }
         // the kernels' occupancy (waves per SIMD as compiled: 3 narrow, 2 wide or coop) sizes the
         // persistent and spread grids (run_nfa)
         int nb = 0;

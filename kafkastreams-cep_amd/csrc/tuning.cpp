@@ -28,6 +28,8 @@ Tuning tuning_from_env() {
   t.resident_waves = rw > 0 ? (uint32_t)rw : 0u;
   t.no_persist = flag("CEP_NO_PERSIST");
   t.spread = (int)num("CEP_SPREAD", 2);
+  const long iso = num("CEP_ISOLATE", 0);
+  t.isolate = iso > 0 ? (uint32_t)iso : 0u;
   const long nc = num("CEP_NODE_CHUNK", 0), oc = num("CEP_OUT_CHUNK", 0), wc = num("CEP_WALK_CAP", 0);
   t.node_chunk = nc > 0 ? (uint32_t)nc : 0u;
   t.out_chunk = oc > 0 ? (uint32_t)oc : 0u;
@@ -36,6 +38,7 @@ Tuning tuning_from_env() {
   t.job_map = (uint32_t)num("CEP_JOB_MAP", 0);
   t.prof = flag("CEP_PROF");
   t.stream_narrow = flag("CEP_STREAM_NARROW");
+  t.stream_wide = flag("CEP_STREAM_WIDE");
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
   t.no_wm_fold = flag("CEP_NO_WM_FOLD");
   const long pf = num("CEP_STENCIL_PF", 0);

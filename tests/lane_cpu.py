@@ -25,13 +25,23 @@ BUILD = os.path.join(os.environ.get("TMPDIR", "/tmp"), "cep_lane_cpu")
 _libs = {}
 
 
-def build(ir: bytes, source: str | None = None, narrow: bool = False):
+# session.cpp's stream build (cep_internal.h jit_stream_source; the lane driver keeps its own
+# persistent-lane setting)
+STREAM_PREFIX = ("#define CEP_DEWEY_PAIRS 3\n#define CEP_LAYOUT_PAIRS 6\n#define CEP_PUT_LOG 1\n"
+                 "#define CEP_STREAM_STOP 1\n#define CEP_WAVES_EU 3\n")
+
+
+def build(ir: bytes, source: str | None = None, narrow: bool = False, stream: bool = False):
     """Compile the query's kernel (or a group's `source`) for the host; returns the loaded
-    library (cached).  The wide Dewey build (6 pairs) unless `narrow`: the driver re-runs jobs
-    in the same build, while libcep re-runs the narrow build's overflowing jobs in the wide one."""
+    library (cached).  The wide Dewey build (6 pairs) unless `narrow` or `stream`: the driver
+    re-runs jobs in the same build, while libcep re-runs the narrow build's overflowing jobs in
+    the wide one; `stream`: the build libcep's streams run, its stopped keys continued by the
+    wide build (loaded alongside)."""
     # the occupancy attribute is for the GPU compile only (the host has no kernels)
     src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\w+\)\)\)", "", source or N.Query(ir).jit_source)
-    if not narrow:
+    if stream:
+        src = STREAM_PREFIX + src
+    elif not narrow:
         src = "#define CEP_DEWEY_PAIRS 6\n" + src
     # $CEP_LANE_DEFINES="A=1 B=2": tuning knobs of nfa_lane.h for this build (tests of the knobs)
     src = "".join(f"#define {d.replace('=', ' ', 1)}\n" for d in os.environ.get("CEP_LANE_DEFINES", "").split()) + src
@@ -62,16 +72,25 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False):
     lib.lane_n_matches.restype = C.c_uint64
     lib.lane_n_pairs.restype = C.c_uint64
     lib.lane_fetch.argtypes = [C.c_void_p] * 7
+    lib.lane_widened.restype = C.c_uint64
+    lib.lane_set_continuation.argtypes = [C.c_void_p]
+    if stream:
+        wide = build(ir, source)
+        lib.lane_set_continuation(C.cast(wide.lane_continue, C.c_void_p).value)
+        lib._wide = wide
     _libs[key] = lib
     return lib
 
 
 def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bits=True, _group=None, ts=None,
-        narrow=False):
+        narrow=False, wide_stream=False):
     """Same result dict as tests/gpu_helpers.gpu_run (minus the device digest).  streaming:
-    the batch continues the keys' streams of the previous streaming call (reset=False).
-    bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the chunked scan."""
-    lib = build(ir, _group["source"] if _group else None, narrow=narrow)
+    the batch continues the keys' streams of the previous streaming call (reset=False), on the
+    build libcep's streams run (the stream build when the query's versions fit it, unless
+    wide_stream).  bits: quiet lanes use the begin-hit bitmap (as on the GPU) instead of the
+    chunked scan."""
+    stream = streaming and not narrow and not wide_stream and not _group
+    lib = build(ir, _group["source"] if _group else None, narrow=narrow, stream=stream)
     n_q = len(_group["members"]) if _group else 1
     kc = np.ascontiguousarray(_group["literals"], np.int64) if _group else None
     if streaming and reset:
@@ -95,7 +114,7 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bit
     lib.lane_fetch(*[a.ctypes.data for a in (key, emit, off, seq, stage, err, err_seq)])
     m = {"n_matches": nm, "n_pairs": npairs, "key": key, "emit_seq": emit, "pair_off": off,
          "pair_seq": seq, "pair_stage": stage, "err_code": err, "err_seq": err_seq,
-         "retried": retried.value, "bits_used": bool(lib.lane_bits_used())}
+         "retried": retried.value, "bits_used": bool(lib.lane_bits_used()), "widened": lib.lane_widened()}
     st = (C.c_uint64 * 10)()
     lib.lane_stats(st)
     m["stats"] = dict(zip(("events", "records", "walks", "walk_nodes", "pred_scans", "flushes", "chain_steps",

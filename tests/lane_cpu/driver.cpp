@@ -49,6 +49,28 @@ extern "C" int lane_bits_used() { return g_bits_used; }
 
 extern "C" void lane_stream_reset() { g_stream = Stream{}; }
 
+// The wide build's continuation of keys the stream build stopped (KE_WIDEN, session.cpp
+// run_nfa): another build of the same query (tests/lane_cpu.py loads both), run here over the
+// launch's own arguments - the same rings, pools, carry and outputs.
+typedef void (*ContFn)(void* args, uint64_t nslots);
+static ContFn g_cont = nullptr;
+extern "C" void lane_set_continuation(void* fn) { g_cont = reinterpret_cast<ContFn>(fn); }
+extern "C" void lane_continue(void* args, uint64_t nslots) {
+  cep::NfaArgs& a = *static_cast<cep::NfaArgs*>(args);
+  blockDim.x = 256;
+  if (std::getenv("CEP_LANE_WAVES")) {
+    for (uint64_t s = 0; s < nslots; s += 64) emu::run_wave((unsigned)(s / 256), (unsigned)(s % 256), wave_body, &a);
+  } else {
+    for (uint64_t s = 0; s < nslots; s++) {
+      blockIdx.x = (unsigned)(s / 256);
+      threadIdx.x = (unsigned)(s % 256);
+      cep_nfa_jit(a);
+    }
+  }
+}
+static uint64_t g_widened = 0;
+extern "C" uint64_t lane_widened() { return g_widened; }
+
 // the begin-hit bitmap (cep_nfa_bits), one position at a time; absent when the query's begin
 // stage is not a single BEGIN edge (no bits kernel)
 template <class A_>
@@ -175,6 +197,27 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
     a.pred_pool.cap = std::min<uint32_t>(a.pred_pool.cap, (uint32_t)std::atol(e));
   }
   launch(((nk + 63) / 64) * 64 * n_q, rcap, defer);  // (session.cpp: streams defer their walks too)
+  g_widened = 0;
+  if (streaming) {  // keys the stream build stopped: continued by the wide build (g_cont)
+    std::vector<uint32_t> list;
+    for (uint64_t k = 0; k < jobs; k++)
+      if (ks[k].err == KE_WIDEN) list.push_back((uint32_t)k);
+    if (!list.empty()) {
+      if (!g_cont) std::abort();  // (a stream build without its wide build)
+      const uint32_t wc = std::max<uint32_t>(64, kWalkFlush + 3 * rcap);
+      const uint32_t pl = put_log_entries(rcap);
+      std::vector<v4u> walks(walkq_bytes(list.size(), wc, pl) / 16 + 64);
+      scribble(walks.data(), walks.size() * 16);
+      a.walks = walks.data();
+      a.jobs = list.data();
+      a.n_jobs = list.size();
+      a.widen = 1;
+      g_cont(&a, list.size());
+      a.widen = 0;
+      a.jobs = nullptr;
+      g_widened = list.size();
+    }
+  }
   a.node_pool.cap = (uint32_t)nodes.size();
   a.pred_pool.cap = (uint32_t)preds.size();
   *n_retried = 0;

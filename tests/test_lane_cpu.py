@@ -70,6 +70,63 @@ def test_lane_narrow_build_overflow_is_capacity():
     assert over > 0  # (some KAT needs more than 3 pairs: the retry path is exercised on the GPU)
 
 
+@pytest.mark.parametrize("case", ["nfa_skip_till_any", "fuzz8", "fuzz96", "fuzz80"])
+def test_lane_stream_widen(case):
+    """Streams run the stream build (3-pair versions): a key whose versions outgrow them stops
+    before that event, undone (nfa_lane.h stop_event), and the wide build continues it over
+    the same state - per key the same matches and errors as the whole stream in one pass."""
+    import stream_split as SS
+    if case.startswith("fuzz"):
+        seed = int(case[4:])
+        q = random_query(seed)
+        off, cols = random_stream(seed, 60, 14)
+    else:
+        q, off, cols = build_case(case, kats()[case])
+    ir = q.to_ir()
+    r = oracle.run(ir, off, cols)
+    outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0))
+            for b, (ko, cs) in enumerate(SS.split(off, cols, 3, seed=7))]
+    assert sum(o["widened"] for o in outs) > 0
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
+@pytest.mark.parametrize("seed", list(range(3, 160, 16)) + [21, 80, 393, 571])
+def test_lane_stream_forced_stops(seed, monkeypatch):
+    """Stops forced at pseudo-random records mid-event (CEP_TEST_WIDEN: after earlier records'
+    puts, pushes, twin writes and walks), on fuzz queries including the exact-conflict seeds:
+    the undo plus the wide build's continuation equal the oracle."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_TEST_WIDEN=5")
+    q = random_query(seed)
+    ir = q.to_ir()
+    if oracle.compile_check(ir):
+        pytest.skip("reference compile-time exception")
+    off, cols = random_stream(seed, 60, 14)
+    r = oracle.run(ir, off, cols)
+    outs = [lane_cpu.run(ir, ko, cs, rcap=16384, streaming=True, reset=(b == 0))
+            for b, (ko, cs) in enumerate(SS.split(off, cols, 3, seed=seed))]
+    assert sum(o["widened"] for o in outs) > 0
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
+def test_lane_stream_forced_stops_stock(monkeypatch):
+    """The same on the README and config-4 stress queries (twin slots, LDS ring slots)."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_TEST_WIDEN=11")
+    cfg = W.SynthConfig("t", "stock", 60, 500, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    for q in (W.stock_query("readme"), W.any_kleene_query(carry_volume=True)):
+        ir = q.to_ir()
+        r = oracle.run(ir, off, cols, threads=8)
+        outs = [lane_cpu.run(ir, ko, cs, streaming=True, reset=(b == 0))
+                for b, (ko, cs) in enumerate(SS.split(off, cols, 4, seed=4))]
+        assert sum(o["widened"] for o in outs) > 0
+        np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+        assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
 def test_lane_capacity_retry():
     """rcap 2: most keys overflow the run queue and are re-run with walks in place."""
     cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)
