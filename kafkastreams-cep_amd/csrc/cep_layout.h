@@ -145,7 +145,8 @@ struct KeyCarry {
   int32_t err;         // sticky: the exception that stopped the key
   uint32_t err_seq;
   uint32_t bseq;       // KE_WIDEN: sequence number of the batch's first event of the key
-  uint32_t pad[2];
+  uint32_t west;       // lane order: the key's running work estimate (cep_nfa_est, compile.cpp)
+  uint32_t pad;
 };
 
 // ---- per-key state kept between kernel phases

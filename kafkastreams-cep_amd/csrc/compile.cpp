@@ -1000,6 +1000,11 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "#else\n  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n#endif\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
+    // a stream's order is kept steady across its batches (each launch lasts as long as its
+    // heaviest wave: regrouping the keys every batch sums a different maximum each time): the
+    // estimate is blended with the key's earlier ones, 7/8 of the running figure carried
+    o += "  if (A.carry && A.est_blend) {\n    w += (uint64_t)A.carry[k].west - (A.carry[k].west >> 3);\n";
+    o += "    w = w > 0xFFFFFFFFull ? 0xFFFFFFFFull : w;\n    if (lane == 0) A.carry[k].west = (uint32_t)w;\n  }\n";
     o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n";
     // the watermark's second level: the first (at most) 1024 blocks each reduce a strided
     // share of the bitmap blocks' maxima, one atomicMax per block (one per wave of a full

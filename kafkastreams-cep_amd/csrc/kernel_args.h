@@ -58,6 +58,7 @@ struct NfaArgs {
   uint32_t widen;            // streaming: this launch continues the listed jobs the stream build
                              // stopped (KE_WIDEN) from their carried event, output appended
   uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)
+  uint32_t est_blend;        // streams: blend the estimate with the key's running one (KeyCarry.west)
   uint64_t* bhits;           // cep_nfa_bits: bit p = the begin predicate (null folds) is true or
                              // throws at CSR position p (quiet lanes jump to the next set bit)
   uint64_t n_events;         // CSR positions of the batch (bits kernel)

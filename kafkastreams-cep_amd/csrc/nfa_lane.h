@@ -1889,7 +1889,9 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     // lightest key), so the waves of the heaviest keys carry the lightest neighbours
     const uint64_t l = slot % 64;
     uint64_t rank;
-    if (A.spread && w < A.spread_iso) {  // a heavy rank alone in its wave: no divergent neighbours
+    if (A.spread && w >= A.spread) {  // (the grid's last block past the W waves: idle)
+      rank = ~0ull;
+    } else if (A.spread && w < A.spread_iso) {  // a heavy rank alone in its wave: no divergent neighbours
       rank = l == 0 ? w : ~0ull;
     } else if (A.spread) {
       const uint64_t W = A.spread - A.spread_iso, w2 = w - A.spread_iso;

@@ -442,6 +442,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
     if (mode != 0) spread = std::min<uint64_t>(resident / 64, nk);
     snake = mode == 2 ? 1u : 0u;
   }
+  // (a full launch spread over all its waves - every wave led by one of the heaviest keys with
+  // lighter ones beside it - was measured: cfg 3 29.2 -> 48.8 ms, every wave pays the divergence)
   // heavy ranks alone in their waves (measurement knob): only while the rest still fit
   uint32_t iso = 0;
   if (spread && s->tune.isolate) {
@@ -603,6 +605,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     g.order.ensure(4 * nk);
     g.order_tmp.ensure(4 * nk);
     a.est = g.est.as<uint32_t>();
+    a.est_blend = streaming && !s->tune.no_est_blend ? 1u : 0u;  // ($CEP_NO_EST_BLEND: measurement runs)
     HIPCHECK(launch_fn(g.fn_est, a, (nk + 3) / 4, s->stream));  // a wave per key
     a.wmax = nullptr;  // (reduced once; wm_blocks stays set: no other kernel reads it)
     HIPCHECK(sort_keys_by_work(g.est.as<uint32_t>(), g.est_sorted.as<uint32_t>(), g.order_tmp.as<uint32_t>(),

@@ -39,6 +39,7 @@ Tuning tuning_from_env() {
   t.prof = flag("CEP_PROF");
   t.stream_narrow = flag("CEP_STREAM_NARROW");
   t.stream_wide = flag("CEP_STREAM_WIDE");
+  t.no_est_blend = flag("CEP_NO_EST_BLEND");
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
   t.no_wm_fold = flag("CEP_NO_WM_FOLD");
   const long pf = num("CEP_STENCIL_PF", 0);

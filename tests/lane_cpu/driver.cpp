@@ -196,7 +196,17 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
     a.node_pool.cap = std::min<uint32_t>(a.node_pool.cap, (uint32_t)std::atol(e));
     a.pred_pool.cap = std::min<uint32_t>(a.pred_pool.cap, (uint32_t)std::atol(e));
   }
-  launch(((nk + 63) / 64) * 64 * n_q, rcap, defer);  // (session.cpp: streams defer their walks too)
+  // $CEP_LANE_SPREAD: the launch spread over W waves (session.cpp: underfilled launches): wave
+  // w's lane l runs key l * W + w (odd lanes reversed), W = the value, waves past W idle
+  if (const char* sp = std::getenv("CEP_LANE_SPREAD")) {
+    if (n_q == 1) {
+      a.spread = std::strtoull(sp, nullptr, 10);
+      a.spread_snake = 1;
+    }
+  }
+  // (spread: three idle waves past the W, as the grid's last block can hold)
+  launch(a.spread ? (a.spread + 3) * 64 : ((nk + 63) / 64) * 64 * n_q, rcap, defer);  // (streams defer their walks too)
+  a.spread = 0;
   g_widened = 0;
   if (streaming) {  // keys the stream build stopped: continued by the wide build (g_cont)
     std::vector<uint32_t> list;

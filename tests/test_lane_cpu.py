@@ -127,6 +127,27 @@ def test_lane_stream_forced_stops_stock(monkeypatch):
         assert SS.merge(outs) == SS.oracle_per_key(r, off)
 
 
+@pytest.mark.parametrize("streaming", [False, True])
+def test_lane_spread(streaming, monkeypatch):
+    """An underfilled launch spread over W waves (session.cpp run_nfa, NfaArgs.spread): wave w's
+    lane l runs rank l * W + w, odd lanes reversed; the grid's waves past W (its last block)
+    stay idle - a key run by two lanes would corrupt its stream."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_SPREAD", "4")  # 4 waves x 64 lanes >= 200 keys
+    monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")  # (per batch: one lane per key, as session.cpp)
+    cfg = W.SynthConfig("t", "stock", 200, 300, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    if not streaming:
+        lane_cpu.assert_same(lane_cpu.run(ir, off, cols), r, off)
+        return
+    outs = [lane_cpu.run(ir, ko, cs, streaming=True, reset=(b == 0))
+            for b, (ko, cs) in enumerate(SS.split(off, cols, 3, seed=3))]
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
 def test_lane_capacity_retry():
     """rcap 2: most keys overflow the run queue and are re-run with walks in place."""
     cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)
