@@ -67,6 +67,7 @@ struct Tuning {
   uint32_t job_map = 0;         // $CEP_JOB_MAP (nfa_lane.h job_id)
   bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
   bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
+  uint32_t solo_keys = 0;       // $CEP_SOLO_KEYS: kernel groups run the heaviest keys' jobs alone
   bool no_est_blend = false;    // $CEP_NO_EST_BLEND: a stream's lane order from this batch alone
   bool stream_wide = false;     // $CEP_STREAM_WIDE: streams on the wide build even when the stream build holds
   bool stream_no_order = false; // $CEP_STREAM_NO_ORDER

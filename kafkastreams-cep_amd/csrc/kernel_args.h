@@ -55,6 +55,8 @@ struct NfaArgs {
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;
   KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
+  uint32_t solo;             // kernel groups: wave w's lane 0 alone runs job index w < n_jobs (the
+                             // heaviest keys' jobs, session.cpp run_nfa); the other lanes idle
   uint32_t widen;            // streaming: this launch continues the listed jobs the stream build
                              // stopped (KE_WIDEN) from their carried event, output appended
   uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)

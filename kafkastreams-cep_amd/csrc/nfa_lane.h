@@ -154,6 +154,10 @@ constexpr uint32_t kWalkHint = 8;
 #ifndef CEP_STREAM_STOP
 #define CEP_STREAM_STOP 0
 #endif
+// software-pipelined record loads in the record loop (measurement: $CEP_REC_PF at query compile)
+#ifndef CEP_REC_PF
+#define CEP_REC_PF 0
+#endif
 constexpr int32_t kDwFull = kDeweyPairs >= 6 ? KE_CAPACITY : CEP_STREAM_STOP ? KE_WIDEN : KE_RETRY;
 // Node-chain cache (deferred walks only): the nodes this lane made at the current event and
 // at the previous one, up to kCC each, kept in registers so that put()'s predecessor lookup
@@ -385,6 +389,57 @@ struct Lane {
     for (int s = 0; s < F; s++)
       r.fold[s] = Q::kFold32 ? (int64_t)(int32_t)w[1 + s] : (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
   }
+
+#if CEP_REC_PF
+  // software-pipelined record loads (event_records): every quad a record's decode reads, loaded
+  // without a look at the header (the Dewey quads past the record's pairs are masked off at
+  // decode), so record i+1's loads go out before record i's step and land while it runs
+  static constexpr int kRawQ = 1 + Lay::kDwRegQuads + Lay::kFoldQuads;
+  __device__ __forceinline__ void load_raw(uint32_t h, uint32_t slot, v4u* q) const {
+    q[0] = rd(h, slot, 0);
+#pragma unroll
+    for (int k = 0; k < Lay::kDwRegQuads; k++) q[1 + k] = rd(h, slot, 1 + k);
+#pragma unroll
+    for (int k = 0; k < Lay::kFoldQuads; k++) q[1 + Lay::kDwRegQuads + k] = rd(h, slot, 1 + Lay::kDwQuads + k);
+  }
+  __device__ __forceinline__ void decode_raw(const v4u* q, Rec<F>& r, uint32_t pf) const {
+    const v4u hd = q[0];
+    r.stage = hd.x & kStageMask;
+    r.event = hd.y;
+    r.ev_first = hd.z == kPending ? pf : hd.z;
+    r.node = hd.w;
+    r.ver.n = hd.x >> 24;
+#pragma unroll
+    for (int k = 0; k < Lay::kDwRegQuads; k++) {
+      const bool in = (uint32_t)(2 * k) < r.ver.n;
+      const v4u dq = q[1 + k];
+      r.ver.v[2 * k] = in ? (int32_t)dq.x : 0;
+      r.ver.c[2 * k] = in ? dq.y : 0u;
+      if (2 * k + 1 < kDeweyPairs) {
+        r.ver.v[2 * k + 1] = in ? (int32_t)dq.z : 0;
+        r.ver.c[2 * k + 1] = in ? dq.w : 0u;
+      }
+    }
+    uint32_t len = 0;
+#pragma unroll
+    for (int k = 0; k < kDeweyPairs; k++)
+      if ((uint32_t)k < r.ver.n) len += r.ver.c[k];
+    r.ver.len = len;
+    uint32_t w[Lay::kFoldQuads * 4];
+#pragma unroll
+    for (int k = 0; k < Lay::kFoldQuads; k++) {
+      const v4u fq = q[1 + Lay::kDwRegQuads + k];
+      w[4 * k] = fq.x;
+      w[4 * k + 1] = fq.y;
+      w[4 * k + 2] = fq.z;
+      w[4 * k + 3] = fq.w;
+    }
+    r.nullmask = w[0];
+#pragma unroll
+    for (int s = 0; s < F; s++)
+      r.fold[s] = Q::kFold32 ? (int64_t)(int32_t)w[1 + s] : (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
+  }
+#endif
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
                                              uint32_t ev_first, const Dewey& ver0, uint32_t node, int d = 0,
@@ -1151,11 +1206,22 @@ struct Lane {
   // the queued records, one after another (NFA.java:99-107)
   __device__ __forceinline__ void event_records() {
     const uint32_t n = count;
+#if CEP_REC_PF
+    v4u nq[kRawQ];
+    if (n > 0) load_raw(half, 0, nq);
+#endif
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
       CEP_STAT(1);
       v4u raw;
+#if CEP_REC_PF
+      // (the step writes only the other half: record i+1's quads stay as loaded)
+      decode_raw(nq, c, pf_ev);
+      raw = nq[0];
+      if (i + 1 < n) load_raw(half, i + 1, nq);
+#else
       load(half, i, c, pf_ev, 0, nullptr, &raw);
+#endif
       in_slot = i;
       in_info = (c.ver.len & 0xFFFFu) | (raw.x & (kTwin | kTwinT)) | (raw.z == kPending ? kInPend : 0u);
       const int produced = q.step(*this, c);
@@ -1878,7 +1944,10 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   // the coop pages' shuffles (nfa_coop.h) read every lane of the wave, so none may have left.
   bool has = true;
   uint64_t job = 0;
-  if (A.jobs) {
+  if (A.solo) {  // one job per wave, alone (session.cpp: beside the persistent launch)
+    has = slot % 64 == 0 && slot / 64 < A.n_jobs;
+    if (has) job = job_id(A, slot / 64);
+  } else if (A.jobs) {
     if (slot >= A.n_jobs) has = false;
     else job = A.jobs[slot];
   } else {

@@ -213,6 +213,8 @@ struct cep_session {
   cep::Tuning tune{};  // measurement knobs, read once at creation (tuning.cpp)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipStream_t solo_stream = nullptr;  // kernel groups: the solo launch beside the main one
+  hipEvent_t solo_ev0 = nullptr, solo_ev1 = nullptr;
   int cus = 256;  // compute units of the device (persistent-lane grids)
   std::vector<std::unique_ptr<QueryRt>> qs;
   std::vector<std::unique_ptr<GroupRt>> groups;
@@ -451,6 +453,13 @@ void run_nfa(cep_session* s, GroupRt& g) {
     while (iso > 0 && (uint64_t)iso + (spread - iso) * 64 < nk) iso /= 2;
   }
   const uint64_t slots = spread ? spread * 64 : !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
+  // Solo jobs (kernel groups): the jobs of the `solo` heaviest keys by the lane order, each alone
+  // in a wave of its own, launched beside the persistent launch (which claims the rest).  A
+  // group's launch otherwise lasts as long as its heaviest jobs do in waves shared with other
+  // jobs' divergent paths and drains (config 5: the longest wave ~3x the mean); alone, a heavy job
+  // runs its own path only, and the light ones among them finish at once and free their slots.
+  const uint64_t solo_jobs = (persist && g.fn_est && nk > 64) ? std::min<uint64_t>((uint64_t)s->tune.solo_keys, nk / 4) * Q : 0;
+  const uint64_t solo_slots = solo_jobs * 64;
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
@@ -482,7 +491,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   s->preds0.ensure(sizeof(Pred) * node_cap);
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
-  s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
+  s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap) + ring_size(g.F, solo_slots, rcap));
   // deferred walks a key can queue (nfa_lane.h drains at the compiled CEP_WALK_FLUSH, the
   // same value as tune.walk_flush; $CEP_WALK_CAP: tuning)
   // (a stream cannot re-run a key whose event overflows its queue: room for every walk one
@@ -493,7 +502,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // put-log entries per lane: every put one event can log fits twice over (a stream turns a
   // put-log overflow into a sticky error, so it must never happen there)
   uint32_t plog = put_log_entries(rcap);
-  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap, plog));
+  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap, plog) + walkq_size(solo_slots, wcap, plog));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
@@ -626,8 +635,25 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // error - and $CEP_STREAM_NO_ORDER: without the lane order; measurement runs only)
   const bool stream_narrow = s->tune.stream_narrow;
   if (streaming && s->tune.stream_no_order) a.order = nullptr;
+  if (solo_jobs && a.order) {
+    // the solo launch first, on its own stream (after everything above on the session stream);
+    // the persistent lanes claim from the first job past the solo ones
+    NfaArgs b = a;
+    b.job_next = nullptr;
+    b.solo = 1;
+    b.n_jobs = solo_jobs;
+    b.rings = (char*)s->rings.p + ring_size(g.F, std::max<uint64_t>(slots, 1), rcap);
+    b.walks = (char*)s->walks.p + walkq_size(std::max<uint64_t>(slots, 1), wcap, plog);
+    HIPCHECK(hipEventRecord(s->solo_ev0, s->stream));
+    HIPCHECK(hipStreamWaitEvent(s->solo_stream, s->solo_ev0, 0));
+    HIPCHECK(launch_nfa_tier(g, r0.q, b, solo_slots, s->solo_stream, false));
+    HIPCHECK(hipEventRecord(s->solo_ev1, s->solo_stream));
+    HIPCHECK(hipMemsetD32Async((hipDeviceptr_t)&sc->job_next, (int)solo_jobs, 1, s->stream));
+    launches++;
+  }
   if (streaming && g.fn_stream) HIPCHECK(launch_fn(g.fn_stream, a, (slots + 255) / 256, s->stream));
   else HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
+  if (solo_jobs && a.order) HIPCHECK(hipStreamWaitEvent(s->stream, s->solo_ev1, 0));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
   Scratch h{};
@@ -970,6 +996,9 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
     HIPCHECK(hipEventCreate(&s->ev0));
     HIPCHECK(hipEventCreate(&s->ev1));
     HIPCHECK(hipEventCreate(&s->ev2));
+    HIPCHECK(hipStreamCreateWithFlags(&s->solo_stream, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&s->solo_ev0, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&s->solo_ev1, hipEventDisableTiming));
     for (int i = 0; i < n_queries; i++) {
       auto r = std::make_unique<QueryRt>();
       r->q = queries[i];
@@ -1082,6 +1111,9 @@ void cep_session_destroy(cep_session* s) {
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->ev2) (void)hipEventDestroy(s->ev2);
+    if (s->solo_ev0) (void)hipEventDestroy(s->solo_ev0);
+    if (s->solo_ev1) (void)hipEventDestroy(s->solo_ev1);
+    if (s->solo_stream) (void)hipStreamDestroy(s->solo_stream);
     if (s->stream) (void)hipStreamDestroy(s->stream);
   }
   delete s;

@@ -40,6 +40,8 @@ Tuning tuning_from_env() {
   t.stream_narrow = flag("CEP_STREAM_NARROW");
   t.stream_wide = flag("CEP_STREAM_WIDE");
   t.no_est_blend = flag("CEP_NO_EST_BLEND");
+  const long solo = num("CEP_SOLO_KEYS", 0);
+  t.solo_keys = solo > 0 ? (uint32_t)solo : 0u;
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
   t.no_wm_fold = flag("CEP_NO_WM_FOLD");
   const long pf = num("CEP_STENCIL_PF", 0);

@@ -5,7 +5,8 @@
 #      the line's roofline must agree with)
 #   3. separate FETCH_SIZE / WRITE_SIZE passes per workload (profiles/workload.py) -> traffic
 #   4. SQ instruction / cycle counters for cfg 3
-# usage: bash profiles/r04_final.sh <outdir> [parts: bench trace pmc sq]
+#   0. (part `tests`) the GPU suite
+# usage: bash profiles/r04_final.sh <outdir> [parts: tests bench trace pmc sq]
 set -o pipefail
 OUT=${1:-gpurun_out/r04_final}; shift
 PARTS=${@:-bench trace pmc sq}
@@ -13,6 +14,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for P in $PARTS; do
   case $P in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || exit $?
+      ;;
     bench)
       timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.log || exit $?
       ;;

@@ -148,6 +148,21 @@ def test_lane_spread(streaming, monkeypatch):
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
 
 
+@pytest.mark.parametrize("waves", [False, True])
+def test_lane_group_solo(waves, monkeypatch):
+    """Kernel groups with solo jobs (session.cpp run_nfa, NfaArgs.solo): the first keys' jobs
+    one per wave alone, the persistent lanes claiming the rest past them - config 5's variants
+    query by query against the oracle."""
+    monkeypatch.setenv("CEP_LANE_SOLO", "5")
+    if waves:
+        monkeypatch.setenv("CEP_LANE_WAVES", "1")
+    cfg = W.SynthConfig("t", "stock", 40, 400, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    irs = [p.to_ir() for p in W.multi_queries(64)[48:64]]
+    for ir, g in zip(irs, lane_cpu.run_group(irs, off, cols)):
+        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
+
+
 def test_lane_capacity_retry():
     """rcap 2: most keys overflow the run queue and are re-run with walks in place."""
     cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)
