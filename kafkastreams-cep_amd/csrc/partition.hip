@@ -36,21 +36,21 @@ __global__ void __launch_bounds__(256) iota_u32(uint32_t* v, uint64_t n) {
 // key array (and range-checks it) and makes the arrival index from the position; the last
 // writes the sorted keys and the permutation.
 constexpr int kRsThreads = 256, kRsRounds = 32, kRsWaves = kRsThreads / 64;
-constexpr uint64_t kRsTile = (uint64_t)kRsThreads * kRsRounds;  // 8192 events
+constexpr int kRsRoundsMin = 8;  // the smallest tile ($CEP_PART_ROUNDS, partition only)
 constexpr int kRsMaxBits = 8;
 constexpr uint32_t kRsBins = 1u << kRsMaxBits;
 
-template <bool FIRST, bool INV>
+template <bool FIRST, bool INV, int R = kRsRounds>
 __global__ void __launch_bounds__(kRsThreads) rs_hist(const uint32_t* __restrict__ keys, uint64_t n, uint64_t n_keys,
                                                       int shift, int bits, uint32_t* hist, uint64_t T, unsigned* bad) {
   __shared__ uint32_t h[kRsBins];
   const uint32_t bins = 1u << bits, mask = bins - 1;
   for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) h[d] = 0;
   __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+  const uint64_t t0 = (uint64_t)blockIdx.x * ((uint64_t)kRsThreads * R);
   bool oob = false;
 #pragma unroll 8
-  for (int r = 0; r < kRsRounds; r++) {
+  for (int r = 0; r < R; r++) {
     const uint64_t i = t0 + (uint64_t)r * kRsThreads + threadIdx.x;
     if (i < n) {
       const uint32_t k = (FIRST && INV) ? ~keys[i] : keys[i];
@@ -63,34 +63,35 @@ __global__ void __launch_bounds__(kRsThreads) rs_hist(const uint32_t* __restrict
   for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) hist[(uint64_t)d * T + blockIdx.x] = h[d];
 }
 
-template <bool FIRST, bool INV>
+template <bool FIRST, bool INV, int R = kRsRounds>
 __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                          uint64_t n, int shift, int bits,
                                                          const uint32_t* __restrict__ off, uint64_t T, uint32_t* kout,
                                                          uint32_t* vout) {
   __shared__ uint32_t cnt[kRsWaves][kRsBins];  // per-wave digit counts -> the waves' first local slots
   __shared__ uint32_t lstart[kRsBins], gbase[kRsBins];
-  __shared__ uint32_t sk[kRsTile], sv[kRsTile];  // the tile sorted by digit
+  constexpr uint32_t kTile = (uint32_t)kRsThreads * R;
+  __shared__ uint32_t sk[kTile], sv[kTile];  // the tile sorted by digit
   const uint32_t bins = 1u << bits, mask = bins - 1;
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint32_t d = threadIdx.x; d < kRsBins; d += kRsThreads)
 #pragma unroll
     for (int x = 0; x < kRsWaves; x++) cnt[x][d] = 0;
   __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
-  const uint32_t tn = (uint32_t)(n - t0 < kRsTile ? n - t0 : kRsTile);
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint32_t tn = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
   // this wave's events: a contiguous quarter of the tile, 64 per round
-  const uint32_t e0 = w * (uint32_t)(kRsTile / kRsWaves);
+  const uint32_t e0 = w * (kTile / kRsWaves);
   const uint64_t lt = (1ull << lane) - 1ull;
-  uint32_t key[kRsRounds], val[kRsRounds], rank[kRsRounds];
+  uint32_t key[R], val[R], rank[R];
 #pragma unroll
-  for (int r = 0; r < kRsRounds; r++) {
+  for (int r = 0; r < R; r++) {
     const uint32_t i = e0 + (uint32_t)r * 64 + lane;
     key[r] = i < tn ? ((FIRST && INV) ? ~kin[t0 + i] : kin[t0 + i]) : 0u;
     val[r] = i < tn ? (FIRST ? (uint32_t)(t0 + i) : vin[t0 + i]) : 0u;
   }
 #pragma unroll
-  for (int r = 0; r < kRsRounds; r++) {
+  for (int r = 0; r < R; r++) {
     const bool valid = e0 + (uint32_t)r * 64 + lane < tn;
     const uint32_t d = (key[r] >> shift) & mask;
     uint64_t peers = __ballot(valid);
@@ -133,7 +134,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter(const uint32_t* __restr
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kRsRounds; r++) {
+  for (int r = 0; r < R; r++) {
     if (e0 + (uint32_t)r * 64 + lane < tn) {
       const uint32_t p = cnt[w][(key[r] >> shift) & mask] + rank[r];
       sk[p] = key[r];
@@ -170,7 +171,7 @@ __global__ void __launch_bounds__(256) key_offsets(const uint32_t* __restrict__ 
 // tile (b % 8) * per + b / 8, so each XCD walks one contiguous eighth of the CSR positions and
 // its own L2 keeps the arrival-order lines that neighbouring keys share (key k's j-th event
 // sits next to key k+1's).
-constexpr int kGaPer = 8;
+template <int kGaPer>
 __global__ void __launch_bounds__(256) gather_cols(const uint32_t* __restrict__ perm, uint64_t n, int nf, Cols in,
                                                    Cols out, uint32_t wide_mask, const int64_t* ts_in,
                                                    int64_t* ts_out, uint64_t per) {
@@ -215,13 +216,16 @@ static int key_bits(uint64_t n_keys) {
   return b;
 }
 
-static uint64_t rs_tiles(uint64_t n) { return std::max<uint64_t>(1, (n + kRsTile - 1) / kRsTile); }
+static uint64_t rs_tiles(uint64_t n, int rounds = kRsRounds) {
+  const uint64_t t = (uint64_t)kRsThreads * rounds;
+  return std::max<uint64_t>(1, (n + t - 1) / t);
+}
 
 // Device scratch of lsd_sort: bytes needed for n keys of `bits` bits (histograms and their
-// scan, one (key, value) ping-pong pair per intermediate pass).
+// scan, one (key, value) ping-pong pair per intermediate pass), for the smaller tile.
 static size_t lsd_scratch_bytes(uint64_t n, int bits) {
   const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
-  const uint64_t h = (uint64_t)(1u << kRsMaxBits) * rs_tiles(n);
+  const uint64_t h = (uint64_t)(1u << kRsMaxBits) * rs_tiles(n, kRsRoundsMin);
   const uint64_t mid = passes > 1 ? (uint64_t)(passes > 2 ? 2 : 1) * 8 * std::max<uint64_t>(n, 1) : 0;
   return 4 * (2 * h + 256) + mid + 1024;
 }
@@ -229,17 +233,19 @@ static size_t lsd_scratch_bytes(uint64_t n, int bits) {
 // Stable sort of n u32 keys (`bits` significant bits; inv: by ~key, i.e. descending) ->
 // sorted keys (complemented when inv) and the source index of each output position.
 // check_keys > 0: keys >= check_keys set *bad.
-static hipError_t lsd_sort(const uint32_t* key, uint64_t n, int bits, bool inv, uint64_t check_keys,
-                           uint32_t* sorted_keys, uint32_t* perm, void* scratch, size_t scratch_bytes, unsigned* bad,
-                           hipStream_t st) {
+template <int R>
+static hipError_t lsd_sort_r(const uint32_t* key, uint64_t n, int bits, bool inv, uint64_t check_keys,
+                             uint32_t* sorted_keys, uint32_t* perm, void* scratch, size_t scratch_bytes, unsigned* bad,
+                             hipStream_t st) {
   if (!n) return hipSuccess;
   const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
   const int width = (bits + passes - 1) / passes;
-  const uint64_t T = rs_tiles(n);
+  const uint64_t T = rs_tiles(n, R);
   if (lsd_scratch_bytes(n, bits) > scratch_bytes) return hipErrorInvalidValue;
   uint32_t* hist = (uint32_t*)scratch;
   uint32_t* hoff = hist + ((uint64_t)1 << width) * T;
-  uint32_t* mid = (uint32_t*)((char*)scratch + 4 * (2 * (uint64_t)(1u << kRsMaxBits) * T + 256));
+  // (the ping-pong pairs sit past the smaller tile's histograms: the same place for either tile)
+  uint32_t* mid = (uint32_t*)((char*)scratch + 4 * (2 * (uint64_t)(1u << kRsMaxBits) * rs_tiles(n, kRsRoundsMin) + 256));
   uint32_t *mk[2] = {mid, mid + 2 * n}, *mv[2] = {mid + n, mid + 3 * n};
   const uint32_t *ik = key, *iv = nullptr;
   const dim3 g((uint32_t)T), b(kRsThreads);
@@ -250,17 +256,26 @@ static hipError_t lsd_sort(const uint32_t* key, uint64_t n, int bits, bool inv, 
     uint32_t* ok = last ? sorted_keys : mk[p & 1];
     uint32_t* ov = last ? perm : mv[p & 1];
     const uint64_t nk = check_keys ? check_keys : ~0ull;
-    if (p > 0) hipLaunchKernelGGL((rs_hist<false, false>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
-    else if (inv) hipLaunchKernelGGL((rs_hist<true, true>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
-    else hipLaunchKernelGGL((rs_hist<true, false>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    if (p > 0) hipLaunchKernelGGL((rs_hist<false, false, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else if (inv) hipLaunchKernelGGL((rs_hist<true, true, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else hipLaunchKernelGGL((rs_hist<true, false, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
     if ((e = scan_u32(hist, hoff, ((uint64_t)1 << w) * T, st)) != hipSuccess) return e;
-    if (p > 0) hipLaunchKernelGGL((rs_scatter<false, false>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
-    else if (inv) hipLaunchKernelGGL((rs_scatter<true, true>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
-    else hipLaunchKernelGGL((rs_scatter<true, false>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    if (p > 0) hipLaunchKernelGGL((rs_scatter<false, false, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    else if (inv) hipLaunchKernelGGL((rs_scatter<true, true, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
+    else hipLaunchKernelGGL((rs_scatter<true, false, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
     ik = ok;
     iv = ov;
   }
   return hipGetLastError();
+}
+
+static hipError_t lsd_sort(const uint32_t* key, uint64_t n, int bits, bool inv, uint64_t check_keys,
+                           uint32_t* sorted_keys, uint32_t* perm, void* scratch, size_t scratch_bytes, unsigned* bad,
+                           hipStream_t st, int rounds = kRsRounds) {
+  if (rounds == 8) return lsd_sort_r<8>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  if (rounds == 16)
+    return lsd_sort_r<16>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  return lsd_sort_r<kRsRounds>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
 }
 
 // Device scratch of partition(): bytes needed for n events over n_keys keys.
@@ -271,17 +286,27 @@ size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys) { return lsd_scratch
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
-                     hipStream_t st) {
+                     hipStream_t st, int rounds, int gather_per) {
   (void)cnt;
   (void)idx;
-  hipError_t e = lsd_sort(key, n, key_bits(n_keys), false, n_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  hipError_t e =
+      lsd_sort(key, n, key_bits(n_keys), false, n_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st, rounds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(key_offsets, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, st, sorted_keys, n, n_keys,
                      key_off);
   if (n) {
-    const uint64_t tiles = (n + 256 * kGaPer - 1) / (256 * kGaPer), per = (tiles + 7) / 8;
-    hipLaunchKernelGGL(gather_cols, dim3((uint32_t)(8 * per)), dim3(256), 0, st, perm, n, nf, in, out, wide_mask, ts_in,
-                       ts_out, per);
+    // positions per thread ($CEP_GATHER_PER: 4, 8 or 16; measurement runs)
+    const int gp = gather_per == 4 || gather_per == 16 ? gather_per : 8;
+    const uint64_t tiles = (n + 256 * (uint64_t)gp - 1) / (256 * (uint64_t)gp), per = (tiles + 7) / 8;
+    if (gp == 4)
+      hipLaunchKernelGGL(gather_cols<4>, dim3((uint32_t)(8 * per)), dim3(256), 0, st, perm, n, nf, in, out, wide_mask,
+                         ts_in, ts_out, per);
+    else if (gp == 16)
+      hipLaunchKernelGGL(gather_cols<16>, dim3((uint32_t)(8 * per)), dim3(256), 0, st, perm, n, nf, in, out, wide_mask,
+                         ts_in, ts_out, per);
+    else
+      hipLaunchKernelGGL(gather_cols<8>, dim3((uint32_t)(8 * per)), dim3(256), 0, st, perm, n, nf, in, out, wide_mask,
+                         ts_in, ts_out, per);
   }
   return hipGetLastError();
 }

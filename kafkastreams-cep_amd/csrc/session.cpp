@@ -1166,7 +1166,7 @@ static void partition_batch(cep_session* s, const cep_batch* b) {
   HIPCHECK(partition(keys, n, nk, (int)nf, in, out, wide, ts, ts ? s->p_ts.as<int64_t>() : nullptr,
                      s->p_off.as<uint64_t>(), s->p_cnt.as<uint64_t>(), s->p_perm.as<uint32_t>(),
                      s->p_sorted.as<uint32_t>(), s->p_idx.as<uint32_t>(), s->p_scratch.p, sb, &sc->overflow,
-                     s->stream));
+                     s->stream, s->tune.part_rounds, s->tune.gather_per));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   uint32_t bad = 0;
   HIPCHECK(hipMemcpyAsync(&bad, &sc->overflow, sizeof bad, hipMemcpyDeviceToHost, s->stream));
