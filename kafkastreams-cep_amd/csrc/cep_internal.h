@@ -68,7 +68,8 @@ struct Tuning {
   bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
   bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
   int part_rounds = 16;         // $CEP_PART_ROUNDS (8, 16, 32): events per thread of the partition's sort tiles
-  int gather_per = 8;           // $CEP_GATHER_PER (4, 8, 16): CSR positions per thread of the column gather
+  int gather_per = 0;           // $CEP_GATHER_PER (4, 8, 16): the position-order column gather with that many
+                                // positions per thread instead of the key-group tiled one (0)
   uint32_t solo_keys = 0;       // $CEP_SOLO_KEYS: kernel groups run the heaviest keys' jobs alone
   bool no_est_blend = false;    // $CEP_NO_EST_BLEND: a stream's lane order from this batch alone
   bool stream_wide = false;     // $CEP_STREAM_WIDE: streams on the wide build even when the stream build holds
@@ -133,7 +134,7 @@ size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
-                     hipStream_t st, int rounds = 16, int gather_per = 8);
+                     hipStream_t st, int rounds = 16, int gather_per = 0);
 // keys 0..n-1 ordered by est descending -> order (tmp: scratch grown as needed)
 hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st);

@@ -210,6 +210,67 @@ __global__ void __launch_bounds__(256) gather_cols(const uint32_t* __restrict__ 
   }
 }
 
+// The same gather, tiled by key group (round 4): a block owns 32 consecutive keys and walks
+// their events 64 at a time.  Per chunk: each wave reads 8 of the keys' next 64 permutation
+// entries (one contiguous 256 B per key) into LDS; then every thread gathers with lanes laid
+// key-minor - lane l reads key (l mod 32)'s event - so one load instruction touches the 32
+// keys' events of the same index, which sit next to each other when keys arrive interleaved
+// (one 128-B line for a 4-byte column instead of 32); the values go back through LDS and each
+// wave writes its keys' 64 positions contiguously.  Any permutation is gathered exactly; the
+// tiling only decides which loads run together.
+constexpr int kTrKeys = 32, kTrChunk = 64;
+__global__ void __launch_bounds__(256) gather_cols_tr(const uint32_t* __restrict__ perm, const uint64_t* key_off,
+                                                      uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
+                                                      const int64_t* ts_in, int64_t* ts_out) {
+  __shared__ uint32_t s_src[kTrKeys][kTrChunk];
+  __shared__ uint64_t s_val[kTrKeys][kTrChunk + 1];  // (+1: the key-minor stores spread over banks)
+  __shared__ uint64_t s_off[kTrKeys + 1];
+  const uint64_t k0 = (uint64_t)blockIdx.x * kTrKeys;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid <= kTrKeys) s_off[tid] = key_off[k0 + tid < n_keys ? k0 + tid : n_keys];
+  __syncthreads();
+  uint64_t most = 0;
+  for (int k = 0; k < kTrKeys; k++) most = s_off[k + 1] - s_off[k] > most ? s_off[k + 1] - s_off[k] : most;
+  const int nk_cols = nf + (ts_in ? 1 : 0);
+  for (uint64_t c0 = 0; c0 < most; c0 += kTrChunk) {
+    // the chunk's permutation entries: wave w, keys 8w .. 8w+7, lane = event
+#pragma unroll
+    for (int i = 0; i < kTrKeys / 4; i++) {
+      const int k = w * (kTrKeys / 4) + i;
+      const uint64_t j = c0 + (uint64_t)lane;
+      if (s_off[k] + j < s_off[k + 1]) s_src[k][lane] = perm[s_off[k] + j];
+    }
+    __syncthreads();
+    for (int f = 0; f < nk_cols; f++) {
+      const bool is_ts = f == nf;
+      const bool wide = is_ts || ((wide_mask >> f) & 1u);
+      // gather, key-minor: thread t reads key t mod 32, events t / 32 + 8 r
+#pragma unroll
+      for (int r = 0; r < kTrChunk / 8; r++) {
+        const int k = tid % kTrKeys, j = tid / kTrKeys + 8 * r;
+        if (s_off[k] + c0 + (uint64_t)j < s_off[k + 1]) {
+          const uint32_t src = s_src[k][j];
+          s_val[k][j] = is_ts ? (uint64_t)ts_in[src]
+                              : wide ? (uint64_t)((const int64_t*)in.p[f])[src]
+                                     : (uint64_t)(uint32_t)((const int32_t*)in.p[f])[src];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kTrKeys / 4; i++) {
+        const int k = w * (kTrKeys / 4) + i;
+        const uint64_t p = s_off[k] + c0 + (uint64_t)lane;
+        if (p < s_off[k + 1]) {
+          if (is_ts) ts_out[p] = (int64_t)s_val[k][lane];
+          else if (wide) ((int64_t*)out.p[f])[p] = (int64_t)s_val[k][lane];
+          else ((int32_t*)out.p[f])[p] = (int32_t)(uint32_t)s_val[k][lane];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 static int key_bits(uint64_t n_keys) {
   int b = 1;
   while (b < 32 && (1ull << b) < n_keys) b++;
@@ -273,6 +334,10 @@ static hipError_t lsd_sort(const uint32_t* key, uint64_t n, int bits, bool inv, 
                            uint32_t* sorted_keys, uint32_t* perm, void* scratch, size_t scratch_bytes, unsigned* bad,
                            hipStream_t st, int rounds = kRsRounds) {
   if (rounds == 8) return lsd_sort_r<8>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  if (rounds == 12)
+    return lsd_sort_r<12>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
+  if (rounds == 24)
+    return lsd_sort_r<24>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
   if (rounds == 16)
     return lsd_sort_r<16>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
   return lsd_sort_r<kRsRounds>(key, n, bits, inv, check_keys, sorted_keys, perm, scratch, scratch_bytes, bad, st);
@@ -294,7 +359,10 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(key_offsets, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, st, sorted_keys, n, n_keys,
                      key_off);
-  if (n) {
+  if (n && gather_per == 0) {  // the key-group tiled gather (default)
+    hipLaunchKernelGGL(gather_cols_tr, dim3((uint32_t)((n_keys + kTrKeys - 1) / kTrKeys)), dim3(256), 0, st, perm, key_off,
+                       n_keys, nf, in, out, wide_mask, ts_in, ts_out);
+  } else if (n) {
     // positions per thread ($CEP_GATHER_PER: 4, 8 or 16; measurement runs)
     const int gp = gather_per == 4 || gather_per == 16 ? gather_per : 8;
     const uint64_t tiles = (n + 256 * (uint64_t)gp - 1) / (256 * (uint64_t)gp), per = (tiles + 7) / 8;

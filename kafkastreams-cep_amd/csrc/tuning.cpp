@@ -43,9 +43,9 @@ Tuning tuning_from_env() {
   {
     // (measured on cfg 3's arrival order, 1e9 events: 8192-event tiles 48.7 ms, 4096 42.4, 2048 55.8)
     const long r = num("CEP_PART_ROUNDS", 16);
-    t.part_rounds = (r == 8 || r == 32) ? (int)r : 16;
-    const long g = num("CEP_GATHER_PER", 8);
-    t.gather_per = (g == 4 || g == 16) ? (int)g : 8;
+    t.part_rounds = (r == 8 || r == 12 || r == 24 || r == 32) ? (int)r : 16;
+    const long g = num("CEP_GATHER_PER", 0);
+    t.gather_per = (g == 4 || g == 8 || g == 16) ? (int)g : 0;
   }
   const long solo = num("CEP_SOLO_KEYS", 0);
   t.solo_keys = solo > 0 ? (uint32_t)solo : 0u;
