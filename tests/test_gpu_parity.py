@@ -278,6 +278,28 @@ def test_cfg5_group_capacity_retry():
         assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
 
 
+def test_solo_and_isolate_knobs(monkeypatch):
+    """The measurement knobs' launch layouts stay exact: a kernel group with its heaviest keys'
+    jobs alone in waves beside the persistent launch ($CEP_SOLO_KEYS, NfaArgs.solo, a second
+    stream), and an underfilled single-query launch with its heaviest ranks alone in their
+    waves ($CEP_ISOLATE, NfaArgs.spread_iso)."""
+    cfg = W.SynthConfig("t", "stock", 300, 500, 0xCE90000 + 5)
+    off, cols = W.generate(cfg)
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)[48:]]
+    monkeypatch.setenv("CEP_SOLO_KEYS", "8")  # (knobs are read when a session is made)
+    s = N.Session(qs)
+    s.push(off, cols)
+    for i, q in enumerate(qs):
+        assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
+    monkeypatch.delenv("CEP_SOLO_KEYS")
+    monkeypatch.setenv("CEP_ISOLATE", "16")
+    cfg = W.SynthConfig("t", "stock", 2000, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    s = N.Session(N.Query(ir))
+    assert_parity(gpu_run(ir, off, cols, session=s), oracle.run(ir, off, cols, threads=8), off)
+
+
 def test_mixed_session_groups():
     """Queries of different shapes in one session: stock variants share a group, the
     any-Kleene query and the zeroOrMore variant run alone, the strict query on the stencil."""
@@ -509,6 +531,36 @@ def test_streaming_session_batches(query, n_batches, tier):
         m = s.matches(0)
         m["err_code"], m["err_seq"] = s.key_errors(0)
         outs.append(m)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
+@pytest.mark.parametrize("case", ["nfa_skip_till_any", "fuzz8", "fuzz80", "fuzz96"])
+def test_streaming_widen_continuation(case):
+    """Streams run the stream build (3-pair Dewey versions); a key whose versions outgrow it
+    stops before that event and the wide build continues it in the same batch (nfa_lane.h
+    stop_event, session.cpp run_nfa): these queries need 4+ pairs on their streams, and the
+    merged matches and exceptions equal the oracle's single pass."""
+    import stream_split as SS
+    from fuzz_queries import random_query, random_stream
+    from ref_queries import build_case, kats
+    if case.startswith("fuzz"):
+        seed = int(case[4:])
+        q = random_query(seed)
+        off, cols = random_stream(seed, 60, 14)
+    else:
+        q, off, cols = build_case(case, kats()[case])
+    ir = q.to_ir()
+    r = oracle.run(ir, off, cols)
+    s = N.Session(N.Query(ir), streaming=True, max_runs=16384)
+    outs, widened = [], 0
+    for ko, cs in SS.split(off, cols, 3, seed=7):
+        s.push(ko, cs)
+        widened += s.stats(0)["retried_jobs"]
+        m = s.matches(0)
+        m["err_code"], m["err_seq"] = s.key_errors(0)
+        outs.append(m)
+    assert widened > 0
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
     np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
 
