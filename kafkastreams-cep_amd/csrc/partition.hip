@@ -40,27 +40,49 @@ constexpr int kRsRoundsMin = 8;  // the smallest tile ($CEP_PART_ROUNDS, partiti
 constexpr int kRsMaxBits = 8;
 constexpr uint32_t kRsBins = 1u << kRsMaxBits;
 
+// (kRsHistTiles tiles per block, each with its own LDS histogram: 16-B loads, a quarter of the
+// workgroups; one tile per block read the keys at ~3.1 TB/s)
+constexpr int kRsHistTiles = 4;
 template <bool FIRST, bool INV, int R = kRsRounds>
 __global__ void __launch_bounds__(kRsThreads) rs_hist(const uint32_t* __restrict__ keys, uint64_t n, uint64_t n_keys,
                                                       int shift, int bits, uint32_t* hist, uint64_t T, unsigned* bad) {
-  __shared__ uint32_t h[kRsBins];
+  static_assert(R % 4 == 0, "16-B loads");
+  __shared__ uint32_t h[kRsHistTiles][kRsBins];
   const uint32_t bins = 1u << bits, mask = bins - 1;
-  for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) h[d] = 0;
+  for (uint32_t d = threadIdx.x; d < kRsHistTiles * kRsBins; d += kRsThreads) (&h[0][0])[d] = 0;
   __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * ((uint64_t)kRsThreads * R);
   bool oob = false;
-#pragma unroll 8
-  for (int r = 0; r < R; r++) {
-    const uint64_t i = t0 + (uint64_t)r * kRsThreads + threadIdx.x;
-    if (i < n) {
-      const uint32_t k = (FIRST && INV) ? ~keys[i] : keys[i];
-      if (FIRST && !INV && k >= n_keys) oob = true;
-      atomicAdd(&h[(k >> shift) & mask], 1u);
+  const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;  // (a caller's key array may not be)
+  auto add = [&](int t, uint32_t k0) {
+    const uint32_t k = (FIRST && INV) ? ~k0 : k0;
+    if (FIRST && !INV && k >= n_keys) oob = true;
+    atomicAdd(&h[t][(k >> shift) & mask], 1u);
+  };
+#pragma unroll
+  for (int t = 0; t < kRsHistTiles; t++) {
+    const uint64_t tile = (uint64_t)blockIdx.x * kRsHistTiles + t;
+    const uint64_t t0 = tile * ((uint64_t)kRsThreads * R);
+#pragma unroll
+    for (int r = 0; r < R / 4; r++) {
+      const uint64_t i = t0 + ((uint64_t)r * kRsThreads + threadIdx.x) * 4;
+      if (aligned && i + 4 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(keys + i);
+        add(t, v.x);
+        add(t, v.y);
+        add(t, v.z);
+        add(t, v.w);
+      } else {
+        for (uint64_t e = i; e < n && e < i + 4; e++) add(t, keys[e]);
+      }
     }
   }
   if (FIRST && oob) atomicOr(bad, 1u);
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) hist[(uint64_t)d * T + blockIdx.x] = h[d];
+  for (int t = 0; t < kRsHistTiles; t++) {
+    const uint64_t tile = (uint64_t)blockIdx.x * kRsHistTiles + t;
+    if (tile >= T) break;
+    for (uint32_t d = threadIdx.x; d < bins; d += kRsThreads) hist[(uint64_t)d * T + tile] = h[t][d];
+  }
 }
 
 template <bool FIRST, bool INV, int R = kRsRounds>
@@ -309,7 +331,7 @@ static hipError_t lsd_sort_r(const uint32_t* key, uint64_t n, int bits, bool inv
   uint32_t* mid = (uint32_t*)((char*)scratch + 4 * (2 * (uint64_t)(1u << kRsMaxBits) * rs_tiles(n, kRsRoundsMin) + 256));
   uint32_t *mk[2] = {mid, mid + 2 * n}, *mv[2] = {mid + n, mid + 3 * n};
   const uint32_t *ik = key, *iv = nullptr;
-  const dim3 g((uint32_t)T), b(kRsThreads);
+  const dim3 g((uint32_t)T), gh((uint32_t)((T + kRsHistTiles - 1) / kRsHistTiles)), b(kRsThreads);
   hipError_t e = hipSuccess;
   for (int p = 0; p < passes; p++) {
     const int shift = p * width, w = std::min(width, bits - shift);
@@ -317,9 +339,9 @@ static hipError_t lsd_sort_r(const uint32_t* key, uint64_t n, int bits, bool inv
     uint32_t* ok = last ? sorted_keys : mk[p & 1];
     uint32_t* ov = last ? perm : mv[p & 1];
     const uint64_t nk = check_keys ? check_keys : ~0ull;
-    if (p > 0) hipLaunchKernelGGL((rs_hist<false, false, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
-    else if (inv) hipLaunchKernelGGL((rs_hist<true, true, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
-    else hipLaunchKernelGGL((rs_hist<true, false, R>), g, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    if (p > 0) hipLaunchKernelGGL((rs_hist<false, false, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else if (inv) hipLaunchKernelGGL((rs_hist<true, true, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
+    else hipLaunchKernelGGL((rs_hist<true, false, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
     if ((e = scan_u32(hist, hoff, ((uint64_t)1 << w) * T, st)) != hipSuccess) return e;
     if (p > 0) hipLaunchKernelGGL((rs_scatter<false, false, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
     else if (inv) hipLaunchKernelGGL((rs_scatter<true, true, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
