@@ -56,6 +56,7 @@ from __future__ import annotations
 
 import base64
 import json
+import operator
 
 import numpy as np
 
@@ -255,6 +256,11 @@ class CEPProcessor:
         self.max_keys = int(max_keys)
         self.device = device
         self.schema = pattern.schema
+        # the columns of a record value, one C-level getter (process() runs once per record)
+        names = tuple(self.schema.names)
+        self._get_item = operator.itemgetter(*names) if names else (lambda v: ())
+        self._get_attr = operator.attrgetter(*names) if names else (lambda v: ())
+        self._one_col = len(names) == 1
         if self.schema is None:
             raise ValueError("the pattern needs an EventSchema (QueryBuilder(schema))")
         self.ir = pattern.to_ir(semantic_within=semantic_within)  # interns string literals first
@@ -398,9 +404,8 @@ class CEPProcessor:
         S = self.schema
         if S.string_value:
             return (S.encode_literal(value),)
-        if isinstance(value, dict):
-            return tuple(value[n] for n in S.names)
-        return tuple(getattr(value, n) for n in S.names)
+        v = self._get_item(value) if isinstance(value, dict) else self._get_attr(value)
+        return (v,) if self._one_col else v
 
     def flush(self) -> None:
         """Matches the buffered records on the device and forwards the new Sequences."""
