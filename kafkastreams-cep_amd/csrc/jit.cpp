@@ -47,6 +47,25 @@ const char* kHipRuntime = "#pragma once\n";
 
 const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
 
+// compile options: kOpts, then $CEP_JIT_OPTS split on spaces (measurement runs: compiler
+// scheduling strategies and the like; part of the cache key)
+std::vector<std::string> jit_opts() {
+  std::vector<std::string> o(std::begin(kOpts), std::end(kOpts));
+  if (const char* e = std::getenv("CEP_JIT_OPTS")) {
+    std::string cur;
+    for (const char* c = e;; c++) {
+      if (*c == ' ' || *c == 0) {
+        if (!cur.empty()) o.push_back(cur);
+        cur.clear();
+        if (*c == 0) break;
+      } else {
+        cur += *c;
+      }
+    }
+  }
+  return o;
+}
+
 uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   for (unsigned char c : s) {
     h ^= c;
@@ -72,7 +91,7 @@ std::mutex g_mu;
 
 std::string jit_cache_key(const std::string& src) {
   std::string all = src;
-  for (auto o : kOpts) all += o;
+  for (const auto& o : jit_opts()) all += o;
   for (int i = 0; i < kJitHeaderCount; i++) all += kJitHeaderSrcs[i];
   char b[32];
   std::snprintf(b, sizeof b, "%016llx", (unsigned long long)fnv1a(all));
@@ -111,7 +130,10 @@ std::vector<char> jit_code_object(const std::string& src, double* compile_s) {
       HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
   auto t0 = std::chrono::steady_clock::now();
-  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof kOpts / sizeof kOpts[0]), kOpts);
+  const std::vector<std::string> opts = jit_opts();
+  std::vector<const char*> optv;
+  for (const auto& o : opts) optv.push_back(o.c_str());
+  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
   if (compile_s) *compile_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
