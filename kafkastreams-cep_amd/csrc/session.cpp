@@ -458,7 +458,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // group's launch otherwise lasts as long as its heaviest jobs do in waves shared with other
   // jobs' divergent paths and drains (config 5: the longest wave ~3x the mean); alone, a heavy job
   // runs its own path only, and the light ones among them finish at once and free their slots.
-  const uint64_t solo_jobs = (persist && g.fn_est && nk > 64) ? std::min<uint64_t>((uint64_t)s->tune.solo_keys, nk / 4) * Q : 0;
+  // (at most 16384 solo jobs: each holds a 64-lane wave's run queues and walk queue)
+  const uint64_t solo_jobs =
+      (persist && g.fn_est && nk > 64) ? std::min<uint64_t>(std::min<uint64_t>((uint64_t)s->tune.solo_keys, nk / 4) * Q, 16384) : 0;
   const uint64_t solo_slots = solo_jobs * 64;
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));

@@ -6,7 +6,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/r04_solo}
 mkdir -p $OUT
 export TMPDIR=/tmp
-for T in 0 8 24 48; do
+for T in ${SOLO_LIST:-0 8 24 48}; do
   CEP_SOLO_KEYS=$T timeout -k 10 300 python3 profiles/cfg5_probe.py --only 0,3 > $OUT/solo$T.json 2> $OUT/solo$T.log || exit $?
 done
 echo done > $OUT/DONE
