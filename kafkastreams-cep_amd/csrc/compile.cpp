@@ -542,7 +542,7 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // (the drain threshold: session.cpp sizes streams' walk queues by the same tuning value)
   if (tuning_walk_flush() != 24) o += "#define CEP_WALK_FLUSH " + std::to_string(tuning_walk_flush()) + "\n";
   for (const char* knob : {"CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN", "CEP_EST_MODE",
-                           "CEP_REC_PF", "CEP_NO_WALK_SPEC"})
+                           "CEP_REC_PF"})
     if (const char* v = std::getenv(knob))
       if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:

@@ -154,18 +154,6 @@ constexpr uint32_t kWalkHint = 8;
 #ifndef CEP_STREAM_STOP
 #define CEP_STREAM_STOP 0
 #endif
-// Speculative walk loads (kernel groups: config 5's walk-heavy jobs).  A walk's next node is
-// almost always the node made just before the current one (s - 1: a run's nodes come out of the
-// lane's pool chunk in event order; 96-97 % of the hops of config 5's heaviest jobs, 98 % within
-// 4, lane CPU hop statistics): each step loads node s - 1 beside node s, and the next step takes
-// it from registers when it is the one.  ($CEP_NO_WALK_SPEC at query compile: off)
-#ifndef CEP_WALK_SPEC
-#if CEP_WALK_COMPAT2 && !defined(CEP_NO_WALK_SPEC)
-#define CEP_WALK_SPEC 1
-#else
-#define CEP_WALK_SPEC 0
-#endif
-#endif
 // software-pipelined record loads in the record loop (measurement: $CEP_REC_PF at query compile)
 #ifndef CEP_REC_PF
 #define CEP_REC_PF 0
@@ -923,12 +911,8 @@ struct Lane {
   }
 
   // `conf` (deferred walks): set to the node when its delete conflicts with a later put
-  struct WalkSpec {  // CEP_WALK_SPEC: node `s`'s loads, issued one step early (CEP_NONE: none)
-    uint32_t s = CEP_NONE;
-    WalkPre P;
-  };
   __device__ __forceinline__ bool walk_node(uint32_t flags, uint32_t& s, Dewey& w, uint32_t t, uint32_t wid,
-                                            uint32_t& np, uint32_t& conf, WalkSpec* spec = nullptr) {
+                                            uint32_t& np, uint32_t& conf) {
     if (s == CEP_NONE) {
       walk_fail(KE_NPE, t);
       return false;
@@ -937,22 +921,7 @@ struct Lane {
     CEP_PACC(11, 1);
     Node& n = A.nodes[s];
     WalkPre P;
-#if CEP_WALK_SPEC
-    // (the guess was loaded after every store an earlier step made: only a step on node s - 1
-    // itself writes it, and that step takes these quads and guesses again)
-    if (spec && spec->s == s) {
-      P = spec->P;
-    } else {
-      walk_load(s, P);
-    }
-    if (spec) {
-      spec->s = s > 0 ? s - 1 : CEP_NONE;
-      if (s > 0) walk_load(s - 1, spec->P);
-    }
-#else
-    (void)spec;
     walk_load(s, P);
-#endif
     const v4u n0 = P.n0, n1 = P.n1, f0 = P.f0, f1 = P.f1;
     const uint32_t ev_s = n0.x, head = n0.z, lk = n1.z, cur = s;
     uint32_t meta = n1.y;
@@ -1105,9 +1074,6 @@ struct Lane {
     bool active = false, draining = part;
     uint32_t cut = CEP_NONE;   // put-log entry of the first put a walk's delete makes throw
     uint32_t conf = CEP_NONE;  // the node of this step's conflicting delete
-#if CEP_WALK_SPEC
-    WalkSpec spec;
-#endif
 #if CEP_PARTIAL_DRAIN == 1
     const uint32_t n_start = (uint32_t)__popcll(__ballot(part && wq_n > 0));
 #endif
@@ -1160,11 +1126,7 @@ struct Lane {
         active = true;
       }
       CEP_STAT(7);
-#if CEP_WALK_SPEC
-      const bool more = walk_node(flags, s, w, t, id0 + i - 1, np, conf, &spec);
-#else
       const bool more = walk_node(flags, s, w, t, id0 + i - 1, np, conf);
-#endif
       if (conf != CEP_NONE) {
         const uint32_t k = first_put_after(conf, id0 + i - 1);
         conf = CEP_NONE;
