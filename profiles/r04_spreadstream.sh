@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 probe: a streamed batch spread over all its waves ($CEP_SPREAD_STREAM=1: every wave led
 # by one of the heaviest keys, lighter ones beside it) against the lane order.
+# (the knob was removed after this measurement: DESIGN.md §7, round 4)
 # usage: bash profiles/r04_spreadstream.sh <outdir>
 set -o pipefail
 OUT=${1:-gpurun_out/r04_spreadstream}
