@@ -43,8 +43,9 @@ struct NfaArgs {
   uint64_t spread;           // W > 0: an underfilled single-query launch of W waves, wave w's lane l
                              // running rank l * W + w (session.cpp run_nfa); 0: rank w * 64 + l
   uint32_t spread_snake;     // spread: odd lanes take their row of ranks in reverse
-  uint32_t spread_iso;       // spread: the K = spread_iso heaviest ranks run alone, one per wave (waves
-                             // 0..K-1, lane 0); the other ranks spread over waves K..W-1
+  uint32_t spread_iso;       // the K = spread_iso heaviest ranks run alone, one per wave (waves 0..K-1,
+                             // lane 0); the other ranks spread over waves K..W-1 (spread) or 64 per
+                             // wave in rank order from wave K (a single query's lane order, n_q 1)
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
   uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)

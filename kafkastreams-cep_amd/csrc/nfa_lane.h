@@ -1965,6 +1965,10 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
     } else if (A.spread) {
       const uint64_t W = A.spread - A.spread_iso, w2 = w - A.spread_iso;
       rank = A.spread_iso + l * W + ((A.spread_snake && (l & 1)) ? W - 1 - w2 : w2);
+    } else if (A.spread_iso && w < A.spread_iso) {  // (lane order) the heaviest ranks alone
+      rank = l == 0 ? w : ~0ull;
+    } else if (A.spread_iso) {
+      rank = A.spread_iso + (w - A.spread_iso) * 64 + l;
     } else {
       rank = (w / nq) * 64 + l;
     }

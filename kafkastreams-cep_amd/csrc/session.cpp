@@ -452,7 +452,14 @@ void run_nfa(cep_session* s, GroupRt& g) {
     iso = (uint32_t)std::min<uint64_t>(s->tune.isolate, spread - 1);
     while (iso > 0 && (uint64_t)iso + (spread - iso) * 64 < nk) iso /= 2;
   }
-  const uint64_t slots = spread ? spread * 64 : !persist ? ((nk + 63) / 64) * 64 * Q : grid_for(jobs);
+  // ($CEP_STREAM_ISO=K, measurement runs: a stream's K heaviest keys alone in their waves, the
+  // others 64 per wave in lane order - a streamed batch lasts as long as its heaviest wave)
+  if (!spread && streaming && Q == 1 && s->tune.stream_iso && nk > 64)
+    iso = (uint32_t)std::min<uint64_t>(s->tune.stream_iso, nk / 2);
+  const uint64_t slots = spread ? spread * 64
+                         : iso  ? ((uint64_t)iso + (nk - iso + 63) / 64) * 64
+                         : !persist ? ((nk + 63) / 64) * 64 * Q
+                                    : grid_for(jobs);
   // Solo jobs (kernel groups): the jobs of the `solo` heaviest keys by the lane order, each alone
   // in a wave of its own, launched beside the persistent launch (which claims the rest).  A
   // group's launch otherwise lasts as long as its heaviest jobs do in waves shared with other

@@ -47,6 +47,8 @@ Tuning tuning_from_env() {
     const long g = num("CEP_GATHER_PER", 0);
     t.gather_per = (g == 4 || g == 8 || g == 16) ? (int)g : 0;
   }
+  const long siso = num("CEP_STREAM_ISO", 0);
+  t.stream_iso = siso > 0 ? (uint32_t)siso : 0u;
   const long solo = num("CEP_SOLO_KEYS", 0);
   t.solo_keys = solo > 0 ? (uint32_t)solo : 0u;
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");

@@ -260,6 +260,12 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
       cep_nfa_jit(a);
     }
     a.job_next = nullptr;
+  } else if (const char* si = std::getenv("CEP_LANE_STREAM_ISO"); si && streaming && n_q == 1 && !a.spread) {
+    // (session.cpp $CEP_STREAM_ISO: the first K keys alone in their waves, the rest 64 per wave)
+    const uint64_t k = std::min<uint64_t>(std::strtoull(si, nullptr, 10), nk / 2);
+    a.spread_iso = (uint32_t)k;
+    launch((k + (nk - k + 63) / 64) * 64, rcap, defer);
+    a.spread_iso = 0;
   } else {
     launch(a.spread ? (a.spread + 3) * 64 : ((nk + 63) / 64) * 64 * n_q, rcap, defer);  // (streams defer their walks too)
   }

@@ -163,6 +163,22 @@ def test_lane_group_solo(waves, monkeypatch):
         lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
 
 
+def test_lane_stream_isolated_keys(monkeypatch):
+    """A stream's launch with its first keys alone in their waves and the rest 64 per wave from
+    there (session.cpp $CEP_STREAM_ISO, NfaArgs.spread_iso without spread), in emulated waves."""
+    import stream_split as SS
+    monkeypatch.setenv("CEP_LANE_STREAM_ISO", "7")
+    monkeypatch.setenv("CEP_LANE_WAVES", "1")
+    cfg = W.SynthConfig("t", "stock", 150, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=8)
+    outs = [lane_cpu.run(ir, ko, cs, streaming=True, reset=(b == 0))
+            for b, (ko, cs) in enumerate(SS.split(off, cols, 3, seed=5))]
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+
+
 def test_lane_capacity_retry():
     """rcap 2: most keys overflow the run queue and are re-run with walks in place."""
     cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)
