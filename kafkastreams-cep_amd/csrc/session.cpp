@@ -452,8 +452,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
     iso = (uint32_t)std::min<uint64_t>(s->tune.isolate, spread - 1);
     while (iso > 0 && (uint64_t)iso + (spread - iso) * 64 < nk) iso /= 2;
   }
-  // ($CEP_STREAM_ISO=K, measurement runs: a stream's K heaviest keys alone in their waves, the
-  // others 64 per wave in lane order - a streamed batch lasts as long as its heaviest wave)
+  // A stream launch bigger than the chip: its K heaviest keys (by the lane order's estimate) run
+  // alone in their waves, the others 64 per wave in lane order.  A streamed batch lasts as long as
+  // its heaviest wave, and a heavy key's wave otherwise pays its lighter neighbours' divergent
+  // paths and drains too (streamed cfg 3, main launches: 61.3 -> 43.9 ms at K = 2048;
+  // $CEP_STREAM_ISO=K, 0 off: measurement runs)
   if (!spread && streaming && Q == 1 && s->tune.stream_iso && nk > 64)
     iso = (uint32_t)std::min<uint64_t>(s->tune.stream_iso, nk / 2);
   const uint64_t slots = spread ? spread * 64

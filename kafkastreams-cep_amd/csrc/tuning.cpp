@@ -47,7 +47,9 @@ Tuning tuning_from_env() {
     const long g = num("CEP_GATHER_PER", 0);
     t.gather_per = (g == 4 || g == 8 || g == 16) ? (int)g : 0;
   }
-  const long siso = num("CEP_STREAM_ISO", 0);
+  // (measured on the streamed cfg 3, main launches of 10 batches: 0 61.3 ms, 64 56.3, 256 52.4,
+  // 1024 46.8 (46.5, 46.4), 1536 44.8, 2048 43.9 (44.2, 43.7), 3072 46.0, 4096 47.1; profiles/r04/probes/streamiso)
+  const long siso = num("CEP_STREAM_ISO", 2048);
   t.stream_iso = siso > 0 ? (uint32_t)siso : 0u;
   const long solo = num("CEP_SOLO_KEYS", 0);
   t.solo_keys = solo > 0 ? (uint32_t)solo : 0u;
