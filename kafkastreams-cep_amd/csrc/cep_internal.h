@@ -71,6 +71,7 @@ struct Tuning {
   int gather_per = 0;           // $CEP_GATHER_PER (4, 8, 16): the position-order column gather with that many
                                 // positions per thread instead of the key-group tiled one (0)
   uint32_t stream_iso = 2048;   // $CEP_STREAM_ISO: a stream's heaviest keys alone in their waves (0: off)
+  uint32_t batch_iso = 0;       // $CEP_BATCH_ISO: the same for per-batch single-query launches
   uint32_t solo_keys = 0;       // $CEP_SOLO_KEYS: kernel groups run the heaviest keys' jobs alone
   bool no_est_blend = false;    // $CEP_NO_EST_BLEND: a stream's lane order from this batch alone
   bool stream_wide = false;     // $CEP_STREAM_WIDE: streams on the wide build even when the stream build holds

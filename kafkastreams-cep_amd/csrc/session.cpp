@@ -457,8 +457,11 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // its heaviest wave, and a heavy key's wave otherwise pays its lighter neighbours' divergent
   // paths and drains too (streamed cfg 3, main launches: 61.3 -> 43.9 ms at K = 2048;
   // $CEP_STREAM_ISO=K, 0 off: measurement runs)
-  if (!spread && streaming && Q == 1 && s->tune.stream_iso && nk > 64)
-    iso = (uint32_t)std::min<uint64_t>(s->tune.stream_iso, nk / 2);
+  // ($CEP_BATCH_ISO=K, measurement runs: the same for a per-batch launch)
+  if (!spread && !persist && Q == 1 && nk > 64) {
+    const uint32_t k = streaming ? s->tune.stream_iso : s->tune.batch_iso;
+    if (k) iso = (uint32_t)std::min<uint64_t>(k, nk / 2);
+  }
   const uint64_t slots = spread ? spread * 64
                          : iso  ? ((uint64_t)iso + (nk - iso + 63) / 64) * 64
                          : !persist ? ((nk + 63) / 64) * 64 * Q

@@ -51,6 +51,8 @@ Tuning tuning_from_env() {
   // 1024 46.8 (46.5, 46.4), 1536 44.8, 2048 43.9 (44.2, 43.7), 3072 46.0, 4096 47.1; profiles/r04/probes/streamiso)
   const long siso = num("CEP_STREAM_ISO", 2048);
   t.stream_iso = siso > 0 ? (uint32_t)siso : 0u;
+  const long biso = num("CEP_BATCH_ISO", 0);
+  t.batch_iso = biso > 0 ? (uint32_t)biso : 0u;
   const long solo = num("CEP_SOLO_KEYS", 0);
   t.solo_keys = solo > 0 ? (uint32_t)solo : 0u;
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
