@@ -190,4 +190,15 @@ __host__ __device__ inline uint32_t put_log_entries(uint32_t rcap) {
   return need > kPutLogMin ? (uint32_t)need : kPutLogMin;
 }
 
+// lanes per key of the work-estimate kernel (compile.cpp cep_nfa_est; session.cpp sizes its grid
+// with the same function): a power of two at least the bitmap words a mean key spans, 4..64.  A
+// key's words are read one per lane, so a wave per key left most lanes idle on short keys (a
+// streamed batch: ~100 events, 2-3 words per key)
+__host__ __device__ inline uint32_t est_lanes(uint64_t n_events, uint64_t n_keys) {
+  const uint64_t words = (n_keys ? n_events / n_keys : 0) / 64 + 2;
+  uint32_t g = 4;
+  while (g < 64 && g < words) g <<= 1;
+  return g;
+}
+
 }  // namespace cep

@@ -977,15 +977,19 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "    if (" + predName[d.begin_stage][0] + "(e, f, err, K) || err) return true;\n  }\n  return false;\n}\n";
     // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
     // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
-    // One wave per key, read from the begin-hit bitmap (launched first): a lane per 64-event
-    // word, 1 bit per event instead of the predicate's columns.
+    // Read from the begin-hit bitmap (launched first): a lane per 64-event word, 1 bit per
+    // event instead of the predicate's columns.  (A wave per key: 0.32 ms per streamed batch of
+    // 1M keys, ~100 events each.)
+    // G = est_lanes(...) lanes per key (cep_layout.h), 64 / G keys per wave; every lane stays for
+    // the segmented reductions (a lane past the last key has no events)
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_est(NfaArgs A) {\n";
-    o += "  const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);\n  const uint32_t lane = threadIdx.x & 63;\n";
-    o += "  if (k >= A.n_keys) return;\n";
-    o += "  const uint64_t base = A.key_off[k];\n  const uint32_t n = (uint32_t)(A.key_off[k + 1] - base);\n";
+    o += "  const uint32_t G = est_lanes(A.n_events, A.n_keys);\n";
+    o += "  const uint64_t k = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;\n  const uint32_t lane = threadIdx.x & (G - 1);\n";
+    o += "  const bool kin = k < A.n_keys;\n";
+    o += "  const uint64_t base = kin ? A.key_off[k] : 0;\n  const uint32_t n = kin ? (uint32_t)(A.key_off[k + 1] - base) : 0u;\n";
     o += "  uint64_t w = 0;\n";
     o += "  const uint64_t p1 = base + n;\n";
-    o += "  for (uint64_t wi = (base >> 6) + lane; n > 0 && wi <= ((p1 - 1) >> 6); wi += 64) {\n";
+    o += "  for (uint64_t wi = (base >> 6) + lane; n > 0 && wi <= ((p1 - 1) >> 6); wi += G) {\n";
     o += "    uint64_t bits = A.bhits[wi];\n    const uint64_t s = wi << 6;\n";
     o += "    if (s < base) bits &= ~0ull << (base - s);\n";
     o += "    if (p1 - s < 64) bits &= (1ull << (p1 - s)) - 1ull;\n";
@@ -997,8 +1001,9 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     // (ordering by the span after the first begin hit instead, or by span then mean live
     // runs, was measured: cfg 3 31.5 -> 34.1 / 33.2 ms)
     o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n";
-    o += "  for (int o = 32; o > 0; o >>= 1) {\n    const uint64_t y = __shfl_down(w, o, 64);\n    w = y > w ? y : w;\n  }\n";
-    o += "#else\n  for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o, 64);\n#endif\n";
+    o += "  for (int o = (int)G >> 1; o > 0; o >>= 1) {\n    const uint64_t y = __shfl_down(w, o, (int)G);\n    w = y > w ? y : w;\n  }\n";
+    o += "#else\n  for (int o = (int)G >> 1; o > 0; o >>= 1) w += __shfl_down(w, o, (int)G);\n#endif\n";
+    o += "  if (kin) {\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";
     // a stream's order is kept steady across its batches (each launch lasts as long as its
@@ -1006,12 +1011,12 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     // estimate is blended with the key's earlier ones, 7/8 of the running figure carried
     o += "  if (A.carry && A.est_blend) {\n    w += (uint64_t)A.carry[k].west - (A.carry[k].west >> 3);\n";
     o += "    w = w > 0xFFFFFFFFull ? 0xFFFFFFFFull : w;\n    if (lane == 0) A.carry[k].west = (uint32_t)w;\n  }\n";
-    o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n";
+    o += "  if (lane == 0) A.est[k] = w > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)w;\n  }\n";
     // the watermark's second level: the first (at most) 1024 blocks each reduce a strided
     // share of the bitmap blocks' maxima, one atomicMax per block (one per wave of a full
     // pass cost 10 ms on one word: DESIGN.md)
     o += "  if (A.wmax) {\n    const uint64_t R = gridDim.x < 1024 ? gridDim.x : 1024;\n";
-    o += "    if (blockIdx.x < R && threadIdx.x < 64) {  // (wave 0's key 4 * blockIdx.x < n_keys)\n      int64_t m = INT64_MIN;\n";
+    o += "    if (blockIdx.x < R && threadIdx.x < 64) {\n      int64_t m = INT64_MIN;\n";
     o += "      for (uint64_t i = blockIdx.x + R * (threadIdx.x & 63); i < A.n_wm_blocks; i += R * 64)\n";
     o += "        m = A.wm_blocks[i] > m ? A.wm_blocks[i] : m;\n";
     o += "      for (int o = 32; o > 0; o >>= 1) {\n        const int64_t y = __shfl_down(m, o, 64);\n";

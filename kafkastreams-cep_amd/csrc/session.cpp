@@ -630,7 +630,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
     g.order_tmp.ensure(4 * nk);
     a.est = g.est.as<uint32_t>();
     a.est_blend = streaming && !s->tune.no_est_blend ? 1u : 0u;  // ($CEP_NO_EST_BLEND: measurement runs)
-    HIPCHECK(launch_fn(g.fn_est, a, (nk + 3) / 4, s->stream));  // a wave per key
+    const uint64_t eg = est_lanes(s->n_events, nk);  // lanes per key
+    HIPCHECK(launch_fn(g.fn_est, a, (nk * eg + 255) / 256, s->stream));
     a.wmax = nullptr;  // (reduced once; wm_blocks stays set: no other kernel reads it)
     HIPCHECK(sort_keys_by_work(g.est.as<uint32_t>(), g.est_sorted.as<uint32_t>(), g.order_tmp.as<uint32_t>(),
                                g.order.as<uint32_t>(), nk, g.sort_tmp, g.sort_tmp_bytes, s->stream));
