@@ -137,8 +137,9 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
                      hipStream_t st, int rounds = 16, int gather_per = 0);
-// keys 0..n-1 ordered by est descending -> order (tmp: scratch grown as needed)
-hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
+// keys 0..n-1 ordered by est descending (16-bit sort keys, partition.hip est_key16) -> order;
+// est_sorted: the sorted keys (inverted), key16: n words (tmp: scratch grown as needed)
+hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st);
 std::string jit_cache_key(const std::string& src);
 hipError_t gather_keys(uint64_t n_sel, const uint32_t* sel, const uint64_t* src_off, const uint64_t* dst_off,

@@ -403,10 +403,24 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
 
 // keys by estimated work, longest first (the NFA's lane order, session.cpp): a stable LSD sort
 // by ~est, so equal estimates keep key order
-hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* iota_tmp, uint32_t* order,
+// A work estimate as a 16-bit sort key, monotone in est: exact below 2048, else the exponent and the
+// 11 bits below the leading one (relative step 2^-11).  The lane order only groups like work into
+// waves; two radix passes instead of four (a streamed batch of 1M keys: ~0.15 ms less).
+__global__ void __launch_bounds__(256) est_key16(const uint32_t* __restrict__ est, uint32_t* __restrict__ q, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = est[i];
+  if (x < 2048u) {
+    q[i] = x;
+  } else {
+    const uint32_t e = 31u - (uint32_t)__builtin_clz(x);  // 11..31
+    q[i] = ((e - 10u) << 11) | ((x >> (e - 11u)) & 0x7FFu);
+  }
+}
+
+hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
-  (void)iota_tmp;
-  const size_t need = lsd_scratch_bytes(n, 32);
+  const size_t need = lsd_scratch_bytes(n, 16);
   if (need > tmp_bytes) {
     if (tmp) (void)hipFree(tmp);
     tmp = nullptr;
@@ -415,7 +429,9 @@ hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t
     if (e != hipSuccess) return e;
     tmp_bytes = need;
   }
-  return lsd_sort(est, n, 32, true, 0, est_sorted, order, tmp, tmp_bytes, nullptr, st);
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(est_key16, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, est, key16, n);
+  return lsd_sort(key16, n, 16, true, 0, est_sorted, order, tmp, tmp_bytes, nullptr, st);
 }
 
 }  // namespace cep

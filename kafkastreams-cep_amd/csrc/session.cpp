@@ -1645,17 +1645,18 @@ int cep_lane_balance(cep_session* s, int query, double* ordered, double* identit
   if (!g.est_valid || nk <= 64 || g.est.bytes < 4 * nk) return fail(CEP_E_INVALID, "the last batch ran no work estimate");
   return guarded([&] {
     DeviceGuard dg(s->device);
-    std::vector<uint32_t> est(nk), srt(nk);
+    std::vector<uint32_t> est(nk), ord(nk), srt(nk);
     HIPCHECK(hipMemcpyAsync(est.data(), g.est.p, 4 * nk, hipMemcpyDeviceToHost, s->stream));
-    HIPCHECK(hipMemcpyAsync(srt.data(), g.est_sorted.p, 4 * nk, hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(hipMemcpyAsync(ord.data(), g.order.p, 4 * nk, hipMemcpyDeviceToHost, s->stream));
     HIPCHECK(hipStreamSynchronize(s->stream));
-    auto balance = [&](const std::vector<uint32_t>& v, bool inv) {
+    for (uint64_t i = 0; i < nk; i++) srt[i] = ord[i] < nk ? est[ord[i]] : 0u;  // est in lane order
+    auto balance = [&](const std::vector<uint32_t>& v) {
       double smax = 0, smean = 0;
       for (uint64_t w = 0; w < nk; w += 64) {
         const uint64_t e = std::min<uint64_t>(w + 64, nk);
         double mx = 0, sum = 0;
         for (uint64_t i = w; i < e; i++) {
-          const double x = (double)(inv ? ~v[i] : v[i]);  // the sort keeps ~est (descending)
+          const double x = (double)v[i];
           mx = std::max(mx, x);
           sum += x;
         }
@@ -1664,8 +1665,8 @@ int cep_lane_balance(cep_session* s, int query, double* ordered, double* identit
       }
       return smean > 0 ? smax / smean : 1.0;
     };
-    *ordered = balance(srt, true);
-    *identity = balance(est, false);
+    *ordered = balance(srt);
+    *identity = balance(est);
   });
 }
 
