@@ -109,7 +109,8 @@ void cep_query_destroy(cep_query* q);
 /* The generated C++ of the query's NFA step (what CEP_TIER_JIT compiles), owned by the query. */
 const char* cep_query_jit_source(const cep_query* q);
 /* Compile the query's JIT kernel into the on-disk code-object cache without a GPU
- * ($CEP_JIT_CACHE, default <libcep.so dir>/jit_cache); sessions then load it directly. */
+ * ($CEP_JIT_CACHE, default <libcep.so dir>/jit_cache); sessions then load it directly.  A
+ * cache hit refreshes the entry's mtime (stale entries can be pruned by age). */
 int cep_jit_precompile(const cep_query* q, double* compile_s);
 /* The same for the kernel groups a session over these queries would launch (cep_opts.no_groups
  * = 0): one code object per group of queries that differ only in literals. */

@@ -51,33 +51,26 @@ struct GroupPlan {
 };
 std::vector<GroupPlan> plan_groups(const std::vector<const cep_query*>& qs);
 
-// Measurement knobs ($CEP_* environment variables).  Read once, when a session
-// is created (tuning.cpp) - never on the launch path - and kept in the session.  Results never
-// depend on them; only the launch geometry and the time a batch takes do.
+// Measurement knobs ($CEP_* environment variables).  Read only by the measurement
+// build (libcep_measure.so: CEP_MEASURE, Makefile `measure`), once, when a session is created
+// (tuning.cpp) - never on the launch path - and kept in the session; the release build uses the
+// defaults below.  Results never depend on them; only the launch geometry and the time a batch
+// takes do.
 struct Tuning {
   uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
   bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too
-  int spread = 2;               // $CEP_SPREAD: 0 off, 1 rows in order, 2 odd lanes reversed
-  uint32_t isolate = 0;         // $CEP_ISOLATE: heaviest ranks of a spread launch alone in their waves
+  bool no_spread = false;       // $CEP_NO_SPREAD: underfilled single-query launches not spread
   uint32_t node_chunk = 0;      // $CEP_NODE_CHUNK: pool range per lane (0: default)
   uint32_t out_chunk = 0;       // $CEP_OUT_CHUNK
   uint32_t walk_cap = 0;        // $CEP_WALK_CAP: deferred walks per lane (0: default)
-  uint32_t walk_flush = 24;     // $CEP_WALK_FLUSH: the kernels' drain threshold (compile.cpp
-                                // compiles the same value in)
-  uint32_t job_map = 0;         // $CEP_JOB_MAP (nfa_lane.h job_id)
   bool prof = false;            // $CEP_PROF: print the kernel's time split (compiled in too)
   bool stream_narrow = false;   // $CEP_STREAM_NARROW: streams on the narrow build
-  int part_rounds = 16;         // $CEP_PART_ROUNDS (8, 16, 32): events per thread of the partition's sort tiles
-  int gather_per = 0;           // $CEP_GATHER_PER (4, 8, 16): the position-order column gather with that many
-                                // positions per thread instead of the key-group tiled one (0)
+  int part_rounds = 16;         // $CEP_PART_ROUNDS (8, 12, 16, 24, 32): events per thread of the partition's sort tiles
   uint32_t stream_iso = 2048;   // $CEP_STREAM_ISO: a stream's heaviest keys alone in their waves (0: off)
-  uint32_t batch_iso = 0;       // $CEP_BATCH_ISO: the same for per-batch single-query launches
-  uint32_t solo_keys = 0;       // $CEP_SOLO_KEYS: kernel groups run the heaviest keys' jobs alone
   bool no_est_blend = false;    // $CEP_NO_EST_BLEND: a stream's lane order from this batch alone
   bool stream_wide = false;     // $CEP_STREAM_WIDE: streams on the wide build even when the stream build holds
   bool stream_no_order = false; // $CEP_STREAM_NO_ORDER
   bool no_wm_fold = false;      // $CEP_NO_WM_FOLD: the watermark as its own pass
-  int stencil_pf = 0;           // $CEP_STENCIL_PF: 1, 2 or 4 (0: default)
   bool host_trace = false;      // $CEP_HOST_TRACE: allocations and push phases on stderr
 };
 Tuning tuning_from_env();
@@ -110,7 +103,7 @@ hipError_t launch_digest(uint64_t n, uint32_t arity, const uint16_t* names, cons
 hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n_events, uint32_t* wave_key,
                             uint32_t* zero, uint32_t n_zero, hipStream_t st);
 uint64_t stencil_waves(uint64_t n_events);
-hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, int pf, hipStream_t st);
+hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st);
 uint64_t stencil_tiles(uint64_t n_events);
 hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_off, uint64_t n, int col_width,
                                     void* price, void* volume, int32_t* status, uint32_t* name_span,
@@ -118,7 +111,7 @@ hipError_t launch_decode_stock_json(const uint8_t* bytes, const uint64_t* rec_of
 hipError_t launch_max(const int64_t* ts, uint64_t n, unsigned long long* out, hipStream_t st);
 struct Node;
 hipError_t launch_live_floor(const Node* nodes, uint64_t n_nodes, uint64_t n_keys, uint32_t* floor, hipStream_t st);
-std::vector<char> jit_code_object(const std::string& src, double* compile_s);
+std::vector<char> jit_code_object(const std::string& src, double* compile_s, bool touch = false);
 // the wide build of a generated kernel (6 Dewey pairs; the source as generated is the narrow
 // build): capacity re-runs and streaming sessions run it
 inline std::string jit_wide_source(const std::string& src) { return "#define CEP_DEWEY_PAIRS 6\n" + src; }
@@ -136,7 +129,7 @@ size_t partition_scratch_bytes(uint64_t n, uint64_t n_keys);
 hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, Cols in, Cols out, uint32_t wide_mask,
                      const int64_t* ts_in, int64_t* ts_out, uint64_t* key_off, uint64_t* cnt, uint32_t* perm,
                      uint32_t* sorted_keys, uint32_t* idx, void* scratch, size_t scratch_bytes, unsigned* bad,
-                     hipStream_t st, int rounds = 16, int gather_per = 0);
+                     hipStream_t st, int rounds = 16);
 // keys 0..n-1 ordered by est descending (16-bit sort keys, partition.hip est_key16) -> order;
 // est_sorted: the sorted keys (inverted), key16: n words (tmp: scratch grown as needed)
 hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,

@@ -525,6 +525,110 @@ void usesM(const M* m, std::vector<bool>& fields, bool& ts) {
   usesM(m->b.get(), fields, ts);
 }
 
+// ---- static fold nullness
+// Which fold slots can be null when a queued record is stepped, per dispatch case (the stage a
+// record's epsilon stage proceeds to).  The reference keys fold values by (state, run seq),
+// `get` of an absent one is null (pattern/States.java:46-62), and a record's values come only
+// from the steps that made it (NFA.evaluate, nfa/NFA.java:162-250): a consuming edge applies
+// the stage's aggregates in order (:259-265; an arithmetic fold result is never null, `curr`
+// or `state.get(x)` copies a nullness), a branch copies the current stage's non-null
+// aggregates into an otherwise empty run (ValueStore.branch, pattern/ValueStore.java:92-97),
+// the begin run starts empty (:74-81).  The step as generated (E<stage>) is run abstractly on a
+// may-be-null bitmask over every combination of matched edges, through its PROCEED calls, to a
+// fixpoint over the dispatch cases; a slot that is provably non-null in a case has its null
+// bit masked off at that case's entry, so the compiler drops the unboxing checks (NPE paths)
+// that read it and the exec-mask work around them.  Returns per stage the may-be-null mask of
+// its dispatch case (-1: no queued record reaches it), or an empty vector when the search
+// outgrew its budget (no masking).
+static std::vector<int64_t> fold_nullness(const cep_query* q, const Builder& b) {
+  const DevQuery& d = q->dev;
+  const uint32_t all = d.n_states >= 32 ? ~0u : (1u << d.n_states) - 1u;
+  std::vector<const std::vector<std::pair<uint16_t, std::unique_ptr<Expr>>>*> aggs(d.n_stages, nullptr);
+  for (auto& sa : b.stageAggs) aggs[sa.first] = sa.second;
+  std::vector<int64_t> mn(d.n_stages, -1);
+  long budget = 2000000;
+  auto fold = [&](int st, uint32_t m) {
+    if (!aggs[st]) return m;
+    for (auto& a : *aggs[st]) {
+      const uint32_t bit = 1u << a.first;
+      const Expr* e = a.second.get();
+      if (e->op == 0x09) continue;  // `curr` itself: its own nullness
+      if (e->op == 0x07) m = (m & ~bit) | (((m >> e->idx) & 1u) ? bit : 0u);  // state.get(x): x's
+      else m &= ~bit;  // any operator unboxes its operands (NPE path) and yields a value
+    }
+    return m;
+  };
+  // outcomes of evaluate(cur) on w's mask `m`: (w's mask after, dispatch case of the record that
+  // keeps the run's seq: -1 none, -2 a final match); branch records go straight into `mn`
+  std::function<bool(int, uint32_t, int, std::vector<std::pair<uint32_t, int>>&)> eval =
+      [&](int cur, uint32_t m, int top, std::vector<std::pair<uint32_t, int>>& out) -> bool {
+    const DevStage& S = d.st[cur];
+    for (uint32_t sub = 0; sub < (1u << S.n_edges); sub++) {
+      if (--budget < 0) return false;
+      bool T = false, B = false, I = false, P = false;
+      int bt = -1, pt = -1;
+      for (int e = 0; e < S.n_edges; e++) {
+        if (!((sub >> e) & 1u)) continue;
+        switch (S.e[e].op) {
+          case OP_TAKE: T = true; break;
+          case OP_BEGIN: B = true; bt = S.e[e].target; break;
+          case OP_IGNORE: I = true; break;
+          case OP_PROCEED: P = true; pt = S.e[e].target; break;
+        }
+      }
+      const bool br = (P && T) || (I && T) || (I && B) || (I && P);
+      int same = -1;
+      const auto dispatch = [&](int st) { return d.st[st].type == ST_FINAL ? -2 : st; };
+      if (!br) {
+        if (T) same = cur;
+        else if (B) same = dispatch(bt);
+        else if (I) same = top;
+      } else if (B) {
+        same = dispatch(bt);
+      }
+      std::vector<std::pair<uint32_t, int>> inner;
+      if (P) {
+        if (d.st[pt].type == ST_FINAL) return false;  // (never built: PROCEED targets a pattern stage)
+        if (!eval(pt, m, top, inner)) return false;
+      } else {
+        inner.push_back({m, -1});
+      }
+      for (auto& x : inner) {
+        uint32_t mm = x.first;
+        const int s2 = x.second != -1 ? x.second : same;
+        if (br) {  // the branch record: the current stage's non-null aggregates, nothing else
+          uint32_t bm = all;
+          if (aggs[cur])
+            for (auto& a : *aggs[cur]) bm &= ~(1u << a.first) | (mm & (1u << a.first));
+          mn[cur] = (mn[cur] < 0 ? 0 : mn[cur]) | bm;
+        }
+        if (T || B) mm = fold(cur, mm);
+        if (std::find(out.begin(), out.end(), std::make_pair(mm, s2)) == out.end()) out.push_back({mm, s2});
+      }
+    }
+    return true;
+  };
+  auto run = [&](int st, uint32_t m, int top) {
+    std::vector<std::pair<uint32_t, int>> out;
+    if (!eval(st, m, top, out)) return false;
+    for (auto& x : out)
+      if (x.second >= 0) mn[x.second] = (mn[x.second] < 0 ? 0 : mn[x.second]) | x.first;
+    return true;
+  };
+  // the begin run (a non-epsilon record: no dispatch case; its IGNORE re-adds itself, empty)
+  if (!run((int)d.begin_stage, all, -3)) return {};
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (uint32_t s = 0; s < d.n_stages; s++) {
+      if (mn[s] < 0) continue;
+      const std::vector<int64_t> before = mn;
+      if (!run((int)s, (uint32_t)mn[s], (int)s)) return {};
+      if (mn != before) changed = true;
+    }
+  }
+  return mn;
+}
+
 }  // namespace
 
 static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& lits) {
@@ -538,20 +642,22 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     for (auto& a : *sa.second) uses(a.second.get(), fields, ts);
   std::string o;
   o += "// generated by libcep (compile.cpp generate_jit) — do not edit\n";
-  // tuning knobs of nfa_lane.h / cep_layout.h, for measurement runs only ($CEP_WALK_FLUSH, ...)
-  // (the drain threshold: session.cpp sizes streams' walk queues by the same tuning value)
-  if (tuning_walk_flush() != 24) o += "#define CEP_WALK_FLUSH " + std::to_string(tuning_walk_flush()) + "\n";
-  for (const char* knob : {"CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_CHAIN_CACHE", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN", "CEP_EST_MODE",
-                           "CEP_REC_PF"})
-    if (const char* v = std::getenv(knob))
-      if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   // Dewey RLE pairs held in registers: the kernel as generated is the narrow build (3 pairs:
   // every run of the bench configs fits, SURVEY §8d sample); a job whose version would need
   // more reports KE_RETRY and is re-run by the wide build of the same source (6 pairs:
-  // jit_wide_source), which also runs streaming sessions.  ($CEP_DEWEY_PAIRS: measurement runs)
+  // jit_wide_source), which also runs streaming sessions.
   int narrow = 3;
+#ifdef CEP_MEASURE
+  // tuning knobs of nfa_lane.h / cep_layout.h, measurement builds only (libcep_measure.so,
+  // Makefile `measure`): $CEP_WALK_FLUSH, ..., $CEP_DEWEY_PAIRS.  (The drain threshold is
+  // recorded with the group: session.cpp sizes streams' walk queues by the compiled value.)
+  if (tuning_walk_flush() != 24) o += "#define CEP_WALK_FLUSH " + std::to_string(tuning_walk_flush()) + "\n";
+  for (const char* knob : {"CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_PROF", "CEP_RING_LDS_SLOTS", "CEP_PARTIAL_DRAIN"})
+    if (const char* v = std::getenv(knob))
+      if (std::atoi(v) > 0) o += std::string("#define ") + knob + " " + std::to_string(std::atoi(v)) + "\n";
   if (const char* v = std::getenv("CEP_DEWEY_PAIRS"))
     if (std::atoi(v) > 0) narrow = std::atoi(v);
+#endif
   o += "#ifndef CEP_DEWEY_PAIRS\n#define CEP_DEWEY_PAIRS " + std::to_string(narrow) + "\n";
   // the narrow build re-runs deferred-walk conflicts in the wide one instead of carrying the
   // put log (nfa_lane.h kPutLog)
@@ -559,9 +665,8 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // a single query's narrow build never runs persistent lanes (session.cpp: only kernel groups
   // and the re-runs, which take the wide build, do): its kernel holds run() alone, half the code
   if (!lits.param) o += "#ifndef CEP_PERSIST_LANES\n#define CEP_PERSIST_LANES 0\n#endif\n";
-  // (3 waves per SIMD; 2 with the wave-cooperative record pages, whose capture and resolution
-  // spill ~240 VGPRs at 3: filled in below once kCoop is known)
-  o += "#define CEP_WAVES_EU @@NARROW_WAVES@@\n#endif\n";
+  // (3 waves per SIMD)
+  o += "#define CEP_WAVES_EU 3\n#endif\n";
   // the wide build (6-pair Dewey versions: streams, re-runs) at 2 waves per SIMD: at 3 it
   // spills ~200 B of scratch and ran 20-25 % slower (profiles/r03)
   o += "#ifndef CEP_WAVES_EU\n#define CEP_WAVES_EU 2\n#endif\n";
@@ -662,95 +767,14 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   bool fold32 = true;  // every state a Java int: one word per fold slot in the run record
   for (uint32_t i = 0; i < d.n_states; i++) fold32 = fold32 && d.state_type[i] == 1;
   o += "  static constexpr bool kFold32 = " + std::string(fold32 ? "true" : "false") + ";\n";
-  // run-queue slots in LDS per half ($CEP_RING_LDS caps it, for measurement runs)
+  // run-queue slots in LDS per half ($CEP_RING_LDS caps it: measurement builds)
   std::string rl = "ring_lds_slots<RecLayout<F, kFold32>>()";
+#ifdef CEP_MEASURE
   if (const char* v = std::getenv("CEP_RING_LDS")) rl = "(" + rl + " < " + std::to_string(std::atoi(v)) + " ? " + rl + " : " + std::to_string(std::atoi(v)) + ")";
+#endif
   o += "  static constexpr uint32_t kRingLds = " + rl + ";\n";
   o += "  static constexpr uint32_t begin_stage = " + std::to_string(d.begin_stage) + ";\n";
-  // Wave-cooperative record steps (nfa_coop.h): the static bounds of one queued record's step -
-  // puts, records produced, walks (+ removePattern's) - over the stages a queued record can be
-  // at, and the stage keys it can put.  Needs the begin run in registers, no queued record
-  // putting the begin stage's key, distinct stage keys along every PROCEED chain (a record
-  // puts a stage key at most once per event), and bounds the capture holds; kernel groups
-  // keep the per-lane loop.
-  {
-    struct Bnd {
-      int p = 0, o = 0, w = 0;
-      uint32_t sks = 0;
-      bool ok = true;
-    };
-    // (stage, edge) -> its predicate; a skip_till_next stage's IGNORE is NOT(edge 0's predicate)
-    // (StatesFactory.java:93-96): it never matches together with the consuming edge
-    std::vector<std::vector<const M*>> em(d.n_stages, std::vector<const M*>(3, nullptr));
-    for (auto& pe : b.pending) em[pe.stage][pe.edge] = pe.m.get();
-    std::function<Bnd(int)> bnd = [&](int si) -> Bnd {
-      const DevStage& S = d.st[si];
-      Bnd r;
-      if (S.type == ST_FINAL) return r;
-      bool hT = false, hB = false, hI = false, ignNot = false;
-      int proc = -1;
-      for (int e = 0; e < S.n_edges; e++) {
-        if (S.e[e].op == OP_TAKE) hT = true;
-        if (S.e[e].op == OP_BEGIN) hB = true;
-        if (S.e[e].op == OP_IGNORE) {
-          hI = true;
-          const M* m = em[si][e];
-          ignNot = m && m->k == M::NOT && m->a.get() == em[si][0];
-        }
-        if (S.e[e].op == OP_PROCEED) proc = (int)S.e[e].target;
-      }
-      Bnd t;
-      if (proc >= 0 && proc != si) t = bnd(proc);
-      if (proc == si) t.ok = false;  // (never built: a stage's PROCEED goes to its successor)
-      const bool hP = proc >= 0, cons = hT || hB;
-      const bool canBr = (hP && hT) || (hI && hT && !ignNot) || (hI && hB && !ignNot) || (hI && hP);
-      r.p = (cons ? 1 : 0) + t.p;
-      const int nb = std::max((cons || hI) ? 1 : 0, t.o);
-      const int br = canBr ? (hB ? 1 : 0) + t.o + 1 : 0;
-      r.o = std::max(nb, br);
-      r.w = (canBr ? 1 : 0) + t.w;
-      r.sks = (cons ? 1u << S.sk : 0u) | t.sks;
-      r.ok = t.ok && !(cons && ((t.sks >> S.sk) & 1u));
-      return r;
-    };
-    Bnd all;
-    all.w = 1;  // removePattern
-    for (uint32_t si = 0; si < d.n_stages; si++) {
-      if (si == d.begin_stage || d.st[si].type == ST_FINAL) continue;
-      const Bnd b = bnd((int)si);
-      all.p = std::max(all.p, b.p);
-      all.o = std::max(all.o, b.o);
-      all.w = std::max(all.w, b.w);
-      all.sks |= b.sks;
-      all.ok = all.ok && b.ok;
-    }
-    // Opt-in ($CEP_COOP=1 at query compile): measured slower than the per-lane loop on config 3
-    // (43.1 vs 28.7 ms; the capture and the resolution need 2 waves per SIMD, 3 spill), and no
-    // faster on a lone heavy key (5.45 vs 5.49 ms: its per-event cost is not its record loop),
-    // DESIGN.md §10.1.  The CPU lane tests run the pages on whole emulated waves either way
-    // (tests/lane_cpu sets CEP_COOP_TESTS).
-    const bool want = std::getenv("CEP_COOP") != nullptr;
-    const bool coop = quiet && !lits.param && all.ok && !((all.sks >> bs.sk) & 1u) && all.p <= 4 && all.o <= 4 &&
-                      all.w <= 4;
-    o += std::string("#ifndef CEP_COOP_TESTS\n#define CEP_COOP_TESTS 0\n#endif\n");
-    // (the wide build - 6-pair versions: re-runs, streams - keeps the per-lane loop: its capture
-    // spills ~230 VGPRs at 2 waves per SIMD)
-    o += "  static constexpr bool kCoop = " +
-         std::string(coop ? (want ? "(kDeweyPairs <= 3 || CEP_COOP_TESTS) && !CEP_STREAM_STOP" : "CEP_COOP_TESTS && !CEP_STREAM_STOP") : "false") +
-         ";  // nfa_coop.h\n";
-    o += "  static constexpr int kCoopP = " + std::to_string(std::max(all.p, 1)) + ", kCoopO = " +
-         std::to_string(std::max(all.o, 1)) + ", kCoopW = " + std::to_string(std::max(all.w, 1)) + ";\n";
-    o += "  static constexpr uint32_t kCoopSkMask = " + std::to_string(coop ? all.sks : 0u) + "u;\n";
-    const size_t at = o.find("@@NARROW_WAVES@@");
-    if (at != std::string::npos) o.replace(at, 16, coop && want ? "2" : "3");
-  }
   o += "  typedef Ev EvT;\n";
-  // another lane's event fields (coop pages step other lanes' records)
-  o += "  __device__ __forceinline__ Ev shfl_ev(const Ev& e, uint32_t src) const {\n    Ev r;\n";
-  for (uint32_t f = 0; f < d.n_fields; f++)
-    if (fields[f]) o += "    r.f" + std::to_string(f) + " = __shfl(e.f" + std::to_string(f) + ", src, 64);\n";
-  o += ts ? "    r.ts = __shfl(e.ts, src, 64);\n" : "    r.ts = 0;\n";
-  o += "    return r;\n  }\n";
   o += "  __device__ explicit JitQ(const NfaArgs& a) : A(a) {}\n";
   o += "  __device__ __forceinline__ void set_query(uint32_t qi) { ld_kc(K, A, qi); }\n";
   o += "  __device__ __forceinline__ void load_ev(Ev& e, uint64_t pos) const { ld_ev(e, A, pos); }\n";
@@ -934,12 +958,17 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "    const Top top{c.stage, c.event, c.ev_first, c.node, (c.stage & kRecEps) ? ((c.stage >> 8) & 0xFFu) : kNoSk};\n    Out o{0, -1};\n";
   o += "    const bool brf = (c.stage & kRecBranch) != 0;\n";
   o += "    if (c.stage & kRecEps) {\n      const uint32_t esk = (c.stage >> 8) & 0xFF;\n      switch (c.stage & 0xFF) {\n";
+  const std::vector<int64_t> nullable = fold_nullness(q, b);
+  const uint32_t allStates = d.n_states >= 32 ? ~0u : (1u << d.n_states) - 1u;
   for (uint32_t s = 0; s < d.n_stages; s++) {
     if (d.st[s].type == ST_FINAL) continue;
     const std::string SI = std::to_string(s), SK = std::to_string(d.st[s].sk);
     // (one inlined copy of the stage's code per case: the version is addStage'd first when the
     // record's epsilon stage differs from its target and the run is not branching)
     o += "        case " + SI + ": {\n          Dewey v2 = c.ver;\n";
+    if (!nullable.empty() && nullable[s] >= 0 && ((uint32_t)nullable[s] & allStates) != allStates)
+      o += "          w.nm &= " + std::to_string((uint32_t)nullable[s] | ~allStates) +
+           "u;  // static fold nullness: the other slots are never null here\n";
     o += "          if (esk != " + SK + "u && !brf && !dw_add_stage(v2)) { L.err = kDwFull; return -1; }\n";
     o += "          E" + SI + "(L, top, v2, brf, esk, ev, w, o);\n          break;\n        }\n";
   }
@@ -953,12 +982,14 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   o += "      o.produced++;\n    }\n    return o.produced;\n  }\n};\n\n";
   // Occupancy: the narrow build at 3 waves per SIMD (<= 168 VGPRs; measured best: 2 waves
   // lose ~20 %, 4+ spill to scratch), the wide one at 2 (CEP_WAVES_EU above).
-  // $CEP_JIT_WAVES overrides both for tuning runs (0: compiler's choice).
+  // $CEP_JIT_WAVES overrides both in measurement builds (0: compiler's choice).
   std::string occ = " __attribute__((amdgpu_waves_per_eu(CEP_WAVES_EU)))";
+#ifdef CEP_MEASURE
   if (const char* wv = std::getenv("CEP_JIT_WAVES")) {
     const int waves = std::atoi(wv);
     occ = waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : "";
   }
+#endif
   o += "}  // namespace\n\nextern \"C\" __global__ void __launch_bounds__(256)" + occ + " cep_nfa_jit(NfaArgs A) {\n";
   o += "  JitQ q(A);\n";
   o += "  __shared__ v4u ring_lds[JitQ::kRingLds > 0 ? 4 * 2 * JitQ::kRingLds * RecLayout<F, JitQ::kFold32>::kLdsQuads * 64 : 1];\n";
@@ -993,16 +1024,11 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "    uint64_t bits = A.bhits[wi];\n    const uint64_t s = wi << 6;\n";
     o += "    if (s < base) bits &= ~0ull << (base - s);\n";
     o += "    if (p1 - s < 64) bits &= (1ull << (p1 - s)) - 1ull;\n";
-    // ($CEP_EST_MODE=1 at query compile, measurement runs: the span after the first begin hit,
-    // max instead of sum)
     o += "    while (bits) {\n      const uint32_t b = (uint32_t)__builtin_ctzll(bits);\n      bits &= bits - 1ull;\n";
-    o += "      const uint64_t r = n - (uint32_t)(s + b - base);\n";
-    o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n      w = w > r ? w : r;\n#else\n      w += r;\n#endif\n    }\n  }\n";
+    o += "      w += n - (uint32_t)(s + b - base);\n    }\n  }\n";
     // (ordering by the span after the first begin hit instead, or by span then mean live
     // runs, was measured: cfg 3 31.5 -> 34.1 / 33.2 ms)
-    o += "#if defined(CEP_EST_MODE) && CEP_EST_MODE == 1\n";
-    o += "  for (int o = (int)G >> 1; o > 0; o >>= 1) {\n    const uint64_t y = __shfl_down(w, o, (int)G);\n    w = y > w ? y : w;\n  }\n";
-    o += "#else\n  for (int o = (int)G >> 1; o > 0; o >>= 1) w += __shfl_down(w, o, (int)G);\n#endif\n";
+    o += "  for (int o = (int)G >> 1; o > 0; o >>= 1) w += __shfl_down(w, o, (int)G);\n";
     o += "  if (kin) {\n";
     o += "  w += n / kQuietChunk + 1;\n";
     o += "  if (A.carry && A.carry[k].live) w += (uint64_t)n * A.carry[k].count;  // a stream's carried runs\n";

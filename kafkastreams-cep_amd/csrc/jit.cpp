@@ -47,10 +47,11 @@ const char* kHipRuntime = "#pragma once\n";
 
 const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
 
-// compile options: kOpts, then $CEP_JIT_OPTS split on spaces (measurement runs: compiler
+// compile options: kOpts, then (measurement builds) $CEP_JIT_OPTS split on spaces (compiler
 // scheduling strategies and the like; part of the cache key)
 std::vector<std::string> jit_opts() {
   std::vector<std::string> o(std::begin(kOpts), std::end(kOpts));
+#ifdef CEP_MEASURE
   if (const char* e = std::getenv("CEP_JIT_OPTS")) {
     std::string cur;
     for (const char* c = e;; c++) {
@@ -63,6 +64,7 @@ std::vector<std::string> jit_opts() {
       }
     }
   }
+#endif
   return o;
 }
 
@@ -98,8 +100,10 @@ std::string jit_cache_key(const std::string& src) {
   return b;
 }
 
-// Returns the gfx950 code object for `src`, from the cache or freshly compiled.
-std::vector<char> jit_code_object(const std::string& src, double* compile_s) {
+// Returns the gfx950 code object for `src`, from the cache or freshly compiled.  `touch`: a
+// cache hit refreshes its entry's mtime (cep_jit_precompile*: tests/precompile_jit.py drops the
+// entries no current query maps to by their mtime).
+std::vector<char> jit_code_object(const std::string& src, double* compile_s, bool touch) {
   std::lock_guard<std::mutex> lk(g_mu);
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + jit_cache_key(src) + ".co";
@@ -109,9 +113,7 @@ std::vector<char> jit_code_object(const std::string& src, double* compile_s) {
     if (f) {
       std::vector<char> co((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
       if (!co.empty()) {
-        // $CEP_JIT_TOUCH (tests/precompile_jit.py only): mark the entry as in use, so the
-        // precompile pass can drop entries no current query maps to
-        if (std::getenv("CEP_JIT_TOUCH")) utime(path.c_str(), nullptr);
+        if (touch) utime(path.c_str(), nullptr);
         return co;
       }
     }

@@ -42,12 +42,11 @@ struct NfaArgs {
                              // null: one job per lane (streaming sessions)
   uint64_t spread;           // W > 0: an underfilled single-query launch of W waves, wave w's lane l
                              // running rank l * W + w (session.cpp run_nfa); 0: rank w * 64 + l
-  uint32_t spread_snake;     // spread: odd lanes take their row of ranks in reverse
-  uint32_t spread_iso;       // the K = spread_iso heaviest ranks run alone, one per wave (waves 0..K-1,
-                             // lane 0); the other ranks spread over waves K..W-1 (spread) or 64 per
-                             // wave in rank order from wave K (a single query's lane order, n_q 1)
+                             // (odd lanes take their row of ranks in reverse)
+  uint32_t spread_iso;       // no spread: the K = spread_iso heaviest ranks run alone, one per wave
+                             // (waves 0..K-1, lane 0), the other ranks 64 per wave in rank order
+                             // from wave K (a stream's lane order, n_q 1)
   uint32_t n_q;              // queries of the launch (a kernel group, compile.cpp plan_groups)
-  uint32_t job_map;          // job index -> (query, key) order (nfa_lane.h job_id; 0 = query-minor)
   const int64_t* kc;         // their literal table, n_q x NKC (group kernels)
   Node* nodes;
   Pred* preds;               // the predecessor pool (a node's second and later pointers)
@@ -56,8 +55,6 @@ struct NfaArgs {
   Pool node_pool, pred_pool, out_pool;
   KeyState* ks;
   KeyCarry* carry;           // streaming: per-key state in/out (null: every key starts fresh)
-  uint32_t solo;             // kernel groups: wave w's lane 0 alone runs job index w < n_jobs (the
-                             // heaviest keys' jobs, session.cpp run_nfa); the other lanes idle
   uint32_t widen;            // streaming: this launch continues the listed jobs the stream build
                              // stopped (KE_WIDEN) from their carried event, output appended
   uint32_t* est;             // cep_nfa_est: per-key work estimate (longest-first lane order)

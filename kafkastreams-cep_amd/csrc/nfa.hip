@@ -42,9 +42,6 @@ struct InterpQ {
   static constexpr bool kBeginReg = false;  // quiet is only known at run time here
   static constexpr bool kFold32 = false;     // fold slots hold any state type
   static constexpr uint32_t kRingLds = 0;    // LDS holds the DevQuery and bytecode: queues in HBM
-  static constexpr bool kCoop = false;       // records stepped per lane (nfa_coop.h needs kBeginReg)
-  static constexpr int kCoopP = 1, kCoopO = 1, kCoopW = 1;
-  static constexpr uint32_t kCoopSkMask = 0;
   struct EvT {};                             // the programs read the columns themselves
 
   __device__ InterpQ(const DevQuery& qq, const uint32_t* c, const NfaArgs& a) : q(qq), code(c), A(a) {

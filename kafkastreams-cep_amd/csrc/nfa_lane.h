@@ -124,9 +124,6 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_WALK_COMPAT2
 #define CEP_WALK_COMPAT2 0
 #endif
-#ifndef CEP_CHAIN_CACHE
-#define CEP_CHAIN_CACHE 0
-#endif
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
 constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
@@ -154,21 +151,7 @@ constexpr uint32_t kWalkHint = 8;
 #ifndef CEP_STREAM_STOP
 #define CEP_STREAM_STOP 0
 #endif
-// software-pipelined record loads in the record loop (measurement: $CEP_REC_PF at query compile)
-#ifndef CEP_REC_PF
-#define CEP_REC_PF 0
-#endif
 constexpr int32_t kDwFull = kDeweyPairs >= 6 ? KE_CAPACITY : CEP_STREAM_STOP ? KE_WIDEN : KE_RETRY;
-// Node-chain cache (deferred walks only): the nodes this lane made at the current event and
-// at the previous one, up to kCC each, kept in registers so that put()'s predecessor lookup
-// and the current event's node lookup need no memory round trip.  Exact: every node of an
-// event is made by the key's own lane during that event, nodes are unique per (stage key,
-// event), and with deferred walks nothing deletes a node between two flushes (a flush
-// invalidates the cache; the conflict stamp is still written).  More than kCC nodes at one
-// event: that event's lookups go to memory.
-constexpr int kCC = CEP_CHAIN_CACHE;
-constexpr int kCCs = kCC > 0 ? kCC : 1;
-static_assert(kCC >= 0 && kCC <= 3, "chain cache: 0..3 entries (stage keys packed in 24 bits)");
 
 // may_alias: quads of Node/Pred are also read and written field by field (Node::refs, ...);
 // without it TBAA lets the compiler reorder the two views of the same bytes
@@ -180,9 +163,6 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4), may_alias));
 #define CEP_LDS_AS __attribute__((address_space(3)))
 #endif
 typedef CEP_LDS_AS v4u lds_v4u;
-}  // namespace cep
-#include "nfa_coop.h"
-namespace cep {
 
 // Twin slots.  A record that a step re-adds unchanged (an IGNORE without a new stage: the
 // reference re-adds the same object, NFA.java:225) at the slot it was read from already sits,
@@ -270,11 +250,7 @@ struct Lane {
   // kInPend (stored ev_first kPending)
   uint32_t in_slot = CEP_NONE, pend_slot = CEP_NONE, in_info = 0;
   uint32_t cur_first = CEP_NONE;  // node chain of event j
-  uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending; coop pages)
-  // chain cache (kCC > 0): packed stage keys (byte k) | count << 24 (> kCC: overflow/invalid)
-  uint32_t cc_pack = (kCC + 1u) << 24, pc_pack = (kCC + 1u) << 24;
-  uint32_t cc_id[kCCs], pc_id[kCCs];
-  uint32_t ev_last = CEP_NONE;  // the event of the last event() call (kCC > 0)
+  uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending)
   int err = KE_OK;
   uint32_t err_seq = 0;
   uint32_t n_matches = 0, n_pairs = 0, out_first = CEP_NONE;
@@ -301,8 +277,8 @@ struct Lane {
 
   __device__ Lane(const NfaArgs& a, Q& qq) : A(a), q(qq) {}
 
-  __device__ __forceinline__ v4u* QP(uint32_t h, uint32_t slot, int quad, v4u* b = nullptr) const {
-    return (b ? b : rb) + ((uint64_t)(h * A.rcap + slot) * Lay::kQuads + quad) * 64;
+  __device__ __forceinline__ v4u* QP(uint32_t h, uint32_t slot, int quad) const {
+    return rb + ((uint64_t)(h * A.rcap + slot) * Lay::kQuads + quad) * 64;
   }
   __device__ __forceinline__ v4u* WQ(uint32_t i, int quad) const {
     return wb + ((uint64_t)i * kWalkQuads + quad) * 64;
@@ -324,17 +300,13 @@ struct Lane {
   __device__ __forceinline__ bool lds_slot(uint32_t slot, int quad) const {
     return kRL > 0 && Lay::in_lds(quad) && slot < kRL;
   }
-  // Another lane's queue (nfa_coop.h steps other keys' records): `d` lanes from this one for
-  // the LDS slots (the lanes of a block are interleaved at 16 B), `b` its HBM base (a stream's
-  // queue lives at its key's position, not its lane's)
-  __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad, int d = 0, v4u* b = nullptr) const {
-    if (lds_slot(slot, quad)) return *(LQ(h, slot, Lay::lds_quad(quad)) + d);
-    return *QP(h, slot, quad, b);
+  __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad) const {
+    if (lds_slot(slot, quad)) return *LQ(h, slot, Lay::lds_quad(quad));
+    return *QP(h, slot, quad);
   }
-  __device__ __forceinline__ void wr(uint32_t h, uint32_t slot, int quad, const v4u& v, int d = 0,
-                                     v4u* b = nullptr) const {
-    if (lds_slot(slot, quad)) *(LQ(h, slot, Lay::lds_quad(quad)) + d) = v;
-    else *QP(h, slot, quad, b) = v;
+  __device__ __forceinline__ void wr(uint32_t h, uint32_t slot, int quad, const v4u& v) const {
+    if (lds_slot(slot, quad)) *LQ(h, slot, Lay::lds_quad(quad)) = v;
+    else *QP(h, slot, quad) = v;
   }
   // streaming: the LDS slots of the queue (half `half`, `count` records) <-> their HBM positions
   __device__ __forceinline__ void lds_spill(bool to_hbm) {
@@ -350,9 +322,8 @@ struct Lane {
 
   // ---------------------------------------------------------------- records
   // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
-  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf, int d = 0,
-                                       v4u* b = nullptr, v4u* raw = nullptr) const {
-    const v4u hd = rd(h, slot, 0, d, b);
+  __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf, v4u* raw = nullptr) const {
+    const v4u hd = rd(h, slot, 0);
     if (raw) *raw = hd;
     r.stage = hd.x & kStageMask;
     r.event = hd.y;
@@ -362,7 +333,7 @@ struct Lane {
 #pragma unroll
     for (int k = 0; k < Lay::kDwRegQuads; k++) {
       v4u dq = {0, 0, 0, 0};
-      if ((uint32_t)(2 * k) < r.ver.n) dq = rd(h, slot, 1 + k, d, b);
+      if ((uint32_t)(2 * k) < r.ver.n) dq = rd(h, slot, 1 + k);
       r.ver.v[2 * k] = (int32_t)dq.x;
       r.ver.c[2 * k] = dq.y;
       if (2 * k + 1 < kDeweyPairs) {
@@ -378,7 +349,7 @@ struct Lane {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++) {
-      const v4u fq = rd(h, slot, 1 + Lay::kDwQuads + k, d, b);
+      const v4u fq = rd(h, slot, 1 + Lay::kDwQuads + k);
       w[4 * k] = fq.x;
       w[4 * k + 1] = fq.y;
       w[4 * k + 2] = fq.z;
@@ -389,73 +360,20 @@ struct Lane {
     for (int s = 0; s < F; s++)
       r.fold[s] = Q::kFold32 ? (int64_t)(int32_t)w[1 + s] : (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
   }
-
-#if CEP_REC_PF
-  // software-pipelined record loads (event_records): every quad a record's decode reads, loaded
-  // without a look at the header (the Dewey quads past the record's pairs are masked off at
-  // decode), so record i+1's loads go out before record i's step and land while it runs
-  static constexpr int kRawQ = 1 + Lay::kDwRegQuads + Lay::kFoldQuads;
-  __device__ __forceinline__ void load_raw(uint32_t h, uint32_t slot, v4u* q) const {
-    q[0] = rd(h, slot, 0);
-#pragma unroll
-    for (int k = 0; k < Lay::kDwRegQuads; k++) q[1 + k] = rd(h, slot, 1 + k);
-#pragma unroll
-    for (int k = 0; k < Lay::kFoldQuads; k++) q[1 + Lay::kDwRegQuads + k] = rd(h, slot, 1 + Lay::kDwQuads + k);
-  }
-  __device__ __forceinline__ void decode_raw(const v4u* q, Rec<F>& r, uint32_t pf) const {
-    const v4u hd = q[0];
-    r.stage = hd.x & kStageMask;
-    r.event = hd.y;
-    r.ev_first = hd.z == kPending ? pf : hd.z;
-    r.node = hd.w;
-    r.ver.n = hd.x >> 24;
-#pragma unroll
-    for (int k = 0; k < Lay::kDwRegQuads; k++) {
-      const bool in = (uint32_t)(2 * k) < r.ver.n;
-      const v4u dq = q[1 + k];
-      r.ver.v[2 * k] = in ? (int32_t)dq.x : 0;
-      r.ver.c[2 * k] = in ? dq.y : 0u;
-      if (2 * k + 1 < kDeweyPairs) {
-        r.ver.v[2 * k + 1] = in ? (int32_t)dq.z : 0;
-        r.ver.c[2 * k + 1] = in ? dq.w : 0u;
-      }
-    }
-    uint32_t len = 0;
-#pragma unroll
-    for (int k = 0; k < kDeweyPairs; k++)
-      if ((uint32_t)k < r.ver.n) len += r.ver.c[k];
-    r.ver.len = len;
-    uint32_t w[Lay::kFoldQuads * 4];
-#pragma unroll
-    for (int k = 0; k < Lay::kFoldQuads; k++) {
-      const v4u fq = q[1 + Lay::kDwRegQuads + k];
-      w[4 * k] = fq.x;
-      w[4 * k + 1] = fq.y;
-      w[4 * k + 2] = fq.z;
-      w[4 * k + 3] = fq.w;
-    }
-    r.nullmask = w[0];
-#pragma unroll
-    for (int s = 0; s < F; s++)
-      r.fold[s] = Q::kFold32 ? (int64_t)(int32_t)w[1 + s] : (int64_t)(((uint64_t)w[3 + 2 * s] << 32) | w[2 + 2 * s]);
-  }
-#endif
 
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
-                                             uint32_t ev_first, const Dewey& ver0, uint32_t node, int d = 0,
-                                             v4u* b = nullptr, uint32_t flags = 0) {
+                                             uint32_t ev_first, const Dewey& ver0, uint32_t node, uint32_t flags = 0) {
     const Dewey ver = dw_pin(ver0);
-    wr(h, slot, 0, v4u{stage | flags | (ver.n << 24), event, ev_first, node}, d, b);
+    wr(h, slot, 0, v4u{stage | flags | (ver.n << 24), event, ev_first, node});
 #pragma unroll
     for (int k = 0; k < Lay::kDwRegQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
         wr(h, slot, 1 + k, v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
                                2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
-                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u}, d, b);
+                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u});
   }
 
-  __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm, int d = 0,
-                                              v4u* b = nullptr) {
+  __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm) {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int i = 0; i < Lay::kFoldQuads * 4; i++) w[i] = 0;
@@ -471,7 +389,7 @@ struct Lane {
     }
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++)
-      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]}, d, b);
+      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]});
   }
 
   // (a record moved to another slot: its twin flags do not hold there)
@@ -514,7 +432,7 @@ struct Lane {
     // when the stored ev_first was kPending: in_info bit kInPend)
     if (keep && slot == in_slot && slot >= kRL && (in_info & kInPend) == 0 && ver.len == (in_info & 0xFFFFu)) {
       if (!(in_info & kTwin)) {  // the output copy is stale: written whole, marked the input's twin
-        store_head(half ^ 1u, slot, stage, event, ef, ver, node, 0, nullptr, kTwin);
+        store_head(half ^ 1u, slot, stage, event, ef, ver, node, kTwin);
         return (int)slot;
       }
       // the output copy already holds it: at most its header's flags, never its folds
@@ -562,21 +480,6 @@ struct Lane {
   }
   __device__ __forceinline__ v4u* PQ(uint32_t p, int k) const { return reinterpret_cast<v4u*>(&PR(p)) + k; }
 
-  // the chain cache's node of stage key sk, CEP_NONE if none (nodes are unique per (sk, event))
-  __device__ __forceinline__ uint32_t cache_find(uint32_t pack, const uint32_t* ids, uint32_t sk) const {
-    uint32_t r = CEP_NONE;
-    const uint32_t n = pack >> 24;
-#pragma unroll
-    for (int k = 0; k < kCC; k++)
-      if ((uint32_t)k < n && ((pack >> (8 * k)) & 0xFFu) == sk) r = ids[k];
-    return r;
-  }
-  __device__ __forceinline__ bool cache_ok(uint32_t pack) const { return kCC > 0 && A.defer && (pack >> 24) <= (uint32_t)kCC; }
-  __device__ __forceinline__ void cache_invalidate() {
-    cc_pack = (kCC + 1u) << 24;
-    pc_pack = (kCC + 1u) << 24;
-  }
-
   // node (sk, event of the chain); CEP_NONE when absent or deleted.  (Pool quads are read as
   // 16-B vectors; v4u is may_alias, so the field writes of the same bytes stay ordered.)
   __device__ __forceinline__ uint32_t lookup(uint32_t sk, uint32_t first) {
@@ -613,17 +516,6 @@ struct Lane {
     *NQ(i, 0) = v4u{j, 1u, p, p};
     *NQ(i, 1) = v4u{cur_first, sk | 0x100u | (1u << 16), 0u, key};
     cur_first = i;
-    if (kCC > 0) {
-      const uint32_t n = cc_pack >> 24;
-      if (n < (uint32_t)kCC) {
-#pragma unroll
-        for (int k = 0; k < kCC; k++)
-          if ((uint32_t)k == n) cc_id[k] = i;
-        cc_pack = (cc_pack & ~(0xFFu << (8 * n)) & 0x00FFFFFFu) | (sk << (8 * n)) | ((n + 1) << 24);
-      } else {
-        cc_pack = (kCC + 1u) << 24;  // this event's lookups go to memory
-      }
-    }
     return i;
   }
 
@@ -644,7 +536,7 @@ struct Lane {
 
   // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
   __device__ __forceinline__ uint32_t put_begin(uint32_t sk, const Dewey& v) {
-    const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
+    const uint32_t c = lookup(sk, cur_first);
     if (c == CEP_NONE) return new_node(sk, CEP_NONE, v);
     // a new TimedKeyValue with one pointer: the node's first-pred slot, rewritten (the node is
     // of the current event: no queued walk can read its old pointers)
@@ -670,7 +562,6 @@ struct Lane {
     }
     uint32_t p;
     if (A.defer && hint != CEP_NONE && prev_sk == hint_sk) p = hint;
-    else if (prev_ev + 1 == j && cache_ok(pc_pack)) p = cache_find(pc_pack, pc_id, prev_sk);
     else p = lookup(prev_sk, prev_first);
     if (p == CEP_NONE) {  // "Cannot find predecessor event"
       err = KE_ILLEGAL_STATE;
@@ -690,7 +581,7 @@ struct Lane {
     // can conflict with it: none is when the queue is empty)
     if (A.defer && wq_n > 0) A.nodes[p].lk = opc;
 #endif
-    const uint32_t c = cache_ok(cc_pack) ? cache_find(cc_pack, cc_id, sk) : lookup(sk, cur_first);
+    const uint32_t c = lookup(sk, cur_first);
     if (c == CEP_NONE) return new_node(sk, p, v);
     append_pred(c, p, v);
     return c;
@@ -1063,7 +954,6 @@ struct Lane {
   __device__ __forceinline__ void flush(bool may_stop = false, bool part = true) {
     CEP_STAT(5);
     if (part && wq_n) {  // this lane's walks may delete its nodes (no other lane's can)
-      if (kCC > 0) cache_invalidate();
       clear_hints();
     }
     const uint32_t id0 = opc - wq_n;
@@ -1178,8 +1068,8 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- one event
-  // event() = event_pre(), the records (event_records() per lane, or coop_records() over the
-  // wave: nfa_coop.h), event_post(): the begin run, the queue swap and the finals.
+  // event() = event_pre(), the records (event_records()), event_post(): the begin run, the
+  // queue swap and the finals.
   EvT nev;             // the next event's fields, prefetched by event_pre (consumed at the next event)
   bool nmore = false;  // there is a next event
 
@@ -1188,13 +1078,6 @@ struct Lane {
     CEP_PACC(10, 1);
     pf_ev = cur_first;  // node chain of the previous event: resolves kPending
     cur_first = CEP_NONE;
-    if (kCC > 0) {  // the last event() call's nodes are the previous event's if it was j - 1
-      pc_pack = ev_last + 1 == j ? cc_pack : (kCC + 1u) << 24;
-#pragma unroll
-      for (int k = 0; k < kCC; k++) pc_id[k] = cc_id[k];
-      cc_pack = 0;
-      ev_last = j;
-    }
     n_final = 0;
     ocount = 0;
     // prefetch the next event's fields (consumed by the next event)
@@ -1206,22 +1089,11 @@ struct Lane {
   // the queued records, one after another (NFA.java:99-107)
   __device__ __forceinline__ void event_records() {
     const uint32_t n = count;
-#if CEP_REC_PF
-    v4u nq[kRawQ];
-    if (n > 0) load_raw(half, 0, nq);
-#endif
     for (uint32_t i = 0; i < n; i++) {
       Rec<F> c;
       CEP_STAT(1);
       v4u raw;
-#if CEP_REC_PF
-      // (the step writes only the other half: record i+1's quads stay as loaded)
-      decode_raw(nq, c, pf_ev);
-      raw = nq[0];
-      if (i + 1 < n) load_raw(half, i + 1, nq);
-#else
-      load(half, i, c, pf_ev, 0, nullptr, &raw);
-#endif
+      load(half, i, c, pf_ev, &raw);
       in_slot = i;
       in_info = (c.ver.len & 0xFFFFu) | (raw.x & (kTwin | kTwinT)) | (raw.z == kPending ? kInPend : 0u);
       const int produced = q.step(*this, c);
@@ -1297,246 +1169,6 @@ struct Lane {
     CEP_PACC(2, te9 - te0);
     if (err) return;
     event_post(begin_hit);
-  }
-
-  // ---------------------------------------------------------------- cooperative records
-  // The records of every lane's current event stepped as one flat list, 64 per page, the side
-  // effects resolved in record order (nfa_coop.h).  Convergent: every lane of the wave calls
-  // it; `act`: this lane's key has an event now (event_pre done).  On return each acting lane's
-  // key is as event_records() would have left it: its next queue half holds the records
-  // produced, its node chain and walk queue hold the puts and walks, err the first exception.
-  __device__ __forceinline__ void coop_records(bool act) {
-    using X_t = RecCtx<F, Q>;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t n_own = act ? count : 0u;
-    const uint32_t incl0 = wave_incl_scan(n_own);
-    const uint32_t excl0 = incl0 - n_own;
-    const uint32_t total = __shfl(incl0, 63, 64);
-    // per stage key a record can put: this key's node of (sk, j) and its last pointer, as earlier
-    // pages left them (CEP_NONE: none yet)
-    uint32_t nodeJ[kMaxStageKeys], tailJ[kMaxStageKeys];
-#pragma unroll
-    for (uint32_t sk = 0; sk < (uint32_t)kMaxStageKeys; sk++) {
-      nodeJ[sk] = CEP_NONE;
-      tailJ[sk] = CEP_NONE;
-    }
-    for (uint32_t pb = 0; pb < total; pb += 64) {  // (wave-uniform)
-      const uint32_t r = pb + lane;
-      const bool valid = r < total;
-      // the owner: the last lane whose records start at or before r (it has records: r < total)
-      uint32_t o = 0;
-#pragma unroll
-      for (uint32_t b = 32; b > 0; b >>= 1) {
-        const uint32_t e = __shfl(excl0, o + b, 64);
-        if (e <= r) o += b;
-      }
-      const uint32_t ex_o = __shfl(excl0, o, 64), n_o = __shfl(n_own, o, 64);
-      const int d = (int)o - (int)lane;
-      v4u* const rb_o = reinterpret_cast<v4u*>(__shfl((unsigned long long)rb, o, 64));
-      // this record's key's lanes in the page, and this lane's own key's lanes (owner role)
-      const uint64_t wseg = valid ? lanes_range(ex_o > pb ? ex_o - pb : 0u, ex_o + n_o - pb < 64 ? ex_o + n_o - pb : 64u)
-                                  : 0ull;
-      const uint64_t oseg = (n_own && excl0 < pb + 64 && excl0 + n_own > pb)
-                                ? lanes_range(excl0 > pb ? excl0 - pb : 0u, excl0 + n_own - pb < 64 ? excl0 + n_own - pb : 64u)
-                                : 0ull;
-      const uint64_t below = lanes_below(lane) & wseg;
-      // the owner's context
-      const uint32_t h_o = __shfl(half, o, 64), j_o = __shfl(j, o, 64), pf_o = __shfl(pf_ev, o, 64);
-      const uint32_t key_o = __shfl(key, o, 64), err_o = __shfl((uint32_t)err, o, 64);
-      X_t X(A);
-      X.ev = q.shfl_ev(ev, o);
-      X.j = j_o;
-      X.base = base;
-      int produced = 0;
-      if (valid && !err_o) {
-        CEP_STAT(1);
-        Rec<F> c;
-        load(h_o, r - ex_o, c, pf_o, d, rb_o);
-        produced = q.step(X, c);
-        if (!X.err && produced == 0)  // removePattern
-          X.walk_remove(q.stage_sk(c.stage), c.event, c.ev_first, c.ver, false, (c.stage & kRecEps) ? c.node : CEP_NONE);
-      }
-      // ---- the first exception of each key: records after it take no effect; its own puts
-      // (their stamps) and walks made before it stand, its records do not
-      const bool stepped = valid && !err_o;
-      const uint64_t eb = __ballot(stepped && X.err != KE_OK);
-      const bool live = stepped && !(eb & below);
-      const bool full = live && X.err == KE_OK;  // records and nodes too
-      bool retry = false;     // a pool or the run queue ran out: the key is re-run (KE_RETRY)
-      bool conflict = false;  // the walk queue or the put log ran out: re-run with walks in place
-      // ---- walks: slots in the owner's queue, in record order
-      const uint32_t wq_n_o = __shfl(wq_n, o, 64), wq_h_o = __shfl(wq_h, o, 64), opc_o = __shfl(opc, o, 64);
-      const uint32_t nw = live ? X.nw : 0u;
-      const uint32_t wi = wave_incl_scan(nw);
-      const uint32_t wlo = low_lane(wseg, lane);
-      const uint32_t wb0 = __shfl(wi, wlo ? wlo - 1 : 0, 64);
-      const uint32_t wbefore = wi - nw - (wlo ? wb0 : 0u);  // walks of the key's earlier records in the page
-      // ---- put stamps (the conflict check, nfa_lane.h): a predecessor found live while walks
-      // are queued, stamped with the key's walk count before the record
-#if CEP_PUT_LOG
-      const uint32_t pl_n_o = __shfl(pl_n, o, 64);
-      uint32_t nst = 0;
-      if (live && A.defer && wq_n_o + wbefore > 0)
-#pragma unroll
-        for (int k = 0; k < X_t::kP; k++)
-          if ((uint32_t)k < X.np && X.p_prev[k] != CEP_NONE) nst++;
-      const uint32_t si = wave_incl_scan(nst);
-      const uint32_t sb0 = __shfl(si, wlo ? wlo - 1 : 0, 64);
-      uint32_t sslot = pl_n_o + si - nst - (wlo ? sb0 : 0u);
-#endif
-      if (live && A.defer && wq_n_o + wbefore > 0) {
-#pragma unroll
-        for (int k = 0; k < X_t::kP; k++)
-          if ((uint32_t)k < X.np && X.p_prev[k] != CEP_NONE) {
-            // (two records of the key may stamp one node in the same page: the later record's
-            // stamp, the larger, is the one the sequential order leaves)
-            atomicMax(&A.nodes[X.p_prev[k]].lk, opc_o + wbefore);
-#if CEP_PUT_LOG
-            if (sslot >= A.plog) conflict = true;
-            else *(PL(sslot) + d) = v4u{X.p_prev[k], opc_o + wbefore, j_o, 0u};
-            sslot++;
-#endif
-          }
-      }
-      // the walks themselves
-      if (nw) {
-#pragma unroll
-        for (int k = 0; k < X_t::kW; k++)
-          if ((uint32_t)k < nw) {
-            const uint32_t idx = wq_n_o + wbefore + (uint32_t)k;
-            if (idx >= A.wcap) {
-              conflict = true;
-            } else {
-              const uint32_t qs = wq_h_o + idx >= A.wcap ? wq_h_o + idx - A.wcap : wq_h_o + idx;
-              const Dewey v = dw_pin(X.w_ver[k]);
-              *(WQ(qs, 0) + d) = v4u{X.w_word[k] | (v.n << 24), X.w_ev[k], X.w_first[k], v.len};
-#pragma unroll
-              for (int q2 = 0; q2 < (kDeweyPairs + 1) / 2; q2++)
-                if ((uint32_t)(2 * q2) < v.n)
-                  *(WQ(qs, 1 + q2) + d) = v4u{(uint32_t)v.v[2 * q2], v.c[2 * q2],
-                                              2 * q2 + 1 < kDeweyPairs ? (uint32_t)v.v[2 * q2 + 1] : 0u,
-                                              2 * q2 + 1 < kDeweyPairs ? v.c[2 * q2 + 1] : 0u};
-              reinterpret_cast<uint32_t*>(WQ(qs, kWalkQuads - 1) + d)[0] = j_o;
-            }
-          }
-      }
-      // ---- puts, one stage key at a time: the key's first putter makes the node (or appends to
-      // the one an earlier page made), every putter takes a pointer linked to the next putter's
-#pragma unroll
-      for (uint32_t sk = 0; sk < (uint32_t)kMaxStageKeys; sk++) {
-        if (!((Q::kCoopSkMask >> sk) & 1u)) continue;
-        bool has = false;
-        uint32_t slot = 0;
-#pragma unroll
-        for (int k = 0; k < X_t::kP; k++)
-          if (full && (uint32_t)k < X.np && X.p_sk[k] == sk) {
-            has = true;
-            slot = (uint32_t)k;
-          }
-        const uint64_t B = __ballot(has);
-        const uint64_t Bs = B & wseg;
-        const bool first = has && !(Bs & lanes_below(lane));
-        const uint32_t exn = __shfl(nodeJ[sk], o, 64), ext = __shfl(tailJ[sk], o, 64);
-        const uint32_t cf_o = __shfl(cur_first, o, 64);
-        uint32_t nd = CEP_NONE, pr = CEP_NONE;
-        if (has) {
-          if (first && exn == CEP_NONE) {
-            nd = pool_take(A.node_pool, ncur, nend);
-            if (nd == CEP_NONE) retry = true;
-            else pr = kPred0 | nd;
-          } else {
-            pr = pool_take(A.pred_pool, pcur, pend);
-            if (pr == CEP_NONE) retry = true;
-          }
-        }
-        const uint32_t mine = first ? (exn != CEP_NONE ? exn : nd) : CEP_NONE;
-        const uint32_t node = __shfl(mine, low_lane(Bs, lane), 64);
-        const uint64_t above = Bs & ~lanes_below(lane + 1);
-        const uint32_t nxt0 = __shfl(pr, low_lane(above, lane), 64);
-        const uint32_t last = __shfl(pr, high_lane(Bs, lane), 64);
-        if (has && !retry && node != CEP_NONE) {
-          const uint32_t nxt = above ? nxt0 : CEP_NONE;
-#pragma unroll
-          for (int k = 0; k < X_t::kP; k++)
-            if ((uint32_t)k == slot) {
-              write_pred(pr, X.p_prev[k], X.p_ver[k], nxt);
-              X.p_node[k] = node;
-            }
-          if (first) {
-            const uint32_t cnt = (uint32_t)__popcll(Bs);
-            if (exn == CEP_NONE) {  // a new node at event j holding the key's putters' pointers
-              *NQ(node, 0) = v4u{j_o, 1u, pr, last};
-              *NQ(node, 1) = v4u{cf_o, sk | 0x100u | (cnt << 16), 0u, key_o};
-            } else {  // appended to the node an earlier page made
-              PR(ext).next = pr;
-              Node& n = A.nodes[node];
-              n.tail = last;
-              n.meta += cnt << 16;
-            }
-          }
-        }
-        // owner role: the key's node of (sk, j), its last pointer, its chain of event j
-        const uint64_t Bo = B & oseg;
-        const uint32_t on = __shfl(mine, low_lane(Bo, lane), 64);
-        const uint32_t ot = __shfl(pr, high_lane(Bo, lane), 64);
-        if (Bo) {
-          if (nodeJ[sk] == CEP_NONE && on != CEP_NONE) cur_first = on;
-          nodeJ[sk] = on;
-          tailJ[sk] = ot;
-        }
-      }
-      // ---- records: slots in the owner's next queue half, in record order
-      const uint32_t no = full ? X.no : 0u;
-      const uint32_t oi = wave_incl_scan(no);
-      const uint32_t ob0 = __shfl(oi, wlo ? wlo - 1 : 0, 64);
-      const uint32_t ocount_o = __shfl(ocount, o, 64);
-      const uint32_t slot0 = ocount_o + oi - no - (wlo ? ob0 : 0u);
-      uint32_t nfin = 0;
-      if (no) {
-        if (slot0 + no > A.rcap) {
-          retry = true;
-          if (A.full) atomicOr(A.full, 1u);
-        } else {
-#pragma unroll
-          for (int k = 0; k < X_t::kO; k++)
-            if ((uint32_t)k < no) {
-              uint32_t nd = X.o_node[k];
-#pragma unroll
-              for (int k2 = 0; k2 < X_t::kP; k2++)
-                if (nd == (kTok | (uint32_t)k2)) nd = X.p_node[k2];
-              store_head(h_o ^ 1u, slot0 + (uint32_t)k, X.o_stage[k], X.o_event[k], X.o_ef[k], X.o_ver[k], nd, d, rb_o);
-              store_folds(h_o ^ 1u, slot0 + (uint32_t)k, X.o_fold[k], X.o_nm[k], d, rb_o);
-              if (X.o_stage[k] & kRecFinal) nfin++;
-            }
-        }
-      }
-      // ---- the owner's key after the page: counts, errors
-      const uint64_t rb = __ballot(retry), cb = __ballot(conflict);
-      const uint32_t olo = low_lane(oseg, lane), ohi = high_lane(oseg, lane);
-      const uint32_t fi = wave_incl_scan(nfin);
-      const uint32_t t_lo_o = __shfl(oi, olo ? olo - 1 : 0, 64), t_hi_o = __shfl(oi, ohi, 64);
-      const uint32_t w_lo_o = __shfl(wi, olo ? olo - 1 : 0, 64), w_hi_o = __shfl(wi, ohi, 64);
-      const uint32_t f_lo_o = __shfl(fi, olo ? olo - 1 : 0, 64), f_hi_o = __shfl(fi, ohi, 64);
-#if CEP_PUT_LOG
-      const uint32_t s_lo_o = __shfl(si, olo ? olo - 1 : 0, 64), s_hi_o = __shfl(si, ohi, 64);
-#endif
-      const uint64_t eo = eb & oseg;
-      const uint32_t ecode = __shfl((uint32_t)X.err, low_lane(eo, lane), 64);
-      if (oseg) {
-        ocount += t_hi_o - (olo ? t_lo_o : 0u);
-        const uint32_t wn = w_hi_o - (olo ? w_lo_o : 0u);
-        wq_n += wn;
-        opc += wn;
-        n_final += f_hi_o - (olo ? f_lo_o : 0u);
-#if CEP_PUT_LOG
-        pl_n += s_hi_o - (olo ? s_lo_o : 0u);
-#endif
-        if (err == KE_OK) {
-          if ((rb | cb) & oseg) err = A.carry ? KE_CAPACITY : ((rb & oseg) ? KE_RETRY : KE_CONFLICT);  // (a stream cannot re-run a key)
-          else if (eo) err = (int)ecode;
-        }
-      }
-    }
   }
 
   // ---------------------------------------------------------------- the key's stream
@@ -1622,19 +1254,6 @@ struct Lane {
     return jj < jn;
   }
 
-  // tick() with the records of the wave's events stepped together (nfa_coop.h).  Convergent:
-  // every lane of the wave, `more` false for a lane whose events are over.
-  __device__ __forceinline__ bool coop_tick(bool more) {
-    bool known = false;
-    const int st = more ? tick_pre(known) : 0;
-    const bool act = st == 2;
-    if (act) event_pre();
-    coop_records(act);
-    if (!act) return st == 1;
-    if (!err) event_post(known);
-    return tick_post();
-  }
-
   __device__ __forceinline__ bool tick() {
     bool known = false;
     const int st = tick_pre(known);
@@ -1709,12 +1328,6 @@ struct Lane {
     jn = j0 + n_ev;
     pa_err = KE_OK;
     bool more = jj < jn;
-#ifdef CEP_HOST_LANES
-    const bool coop = Q::kCoop && A.defer && !cep_host_single_lane();  // (tests/lane_cpu: whole waves only)
-#else
-    const bool coop = Q::kCoop && A.defer;  // (wave-uniform)
-#endif
-    (void)coop;
     while (__any(more)) {
       CEP_PACC(8, more ? 1 : 0);
       CEP_PT(tf0);
@@ -1724,17 +1337,7 @@ struct Lane {
       }
       CEP_PT(tf1);
       CEP_PACC(0, tf1 - tf0);
-      if constexpr (Q::kCoop) {
-#if CEP_PERSIST_LANES
-        if (coop) more = coop_tick(more);
-        else if (more) more = tick();
-#else
-        // (a single query's narrow build: its only launch defers its walks, always coop)
-        more = coop_tick(more);
-#endif
-      } else if (more) {
-        more = tick();
-      }
+      if (more) more = tick();
     }
     CEP_PT(tr1);
     // the final drain, every lane of the wave together (lanes whose walk threw mid-stream take
@@ -1780,10 +1383,6 @@ struct Lane {
     wq_h = 0;
     opc = 0;
     pl_n = 0;
-    if (kCC > 0) {
-      cache_invalidate();
-      ev_last = CEP_NONE;
-    }
     wt_last = CEP_NONE;
     wm0 = wp0 = 0;
     jj = 0;
@@ -1802,21 +1401,11 @@ struct Lane {
 };
 
 // job index -> (query, key) job id: explicit (retries) or query-minor over the lane order
-// (job_map 1, measurement runs: a wave = 8 queries x 8 keys of similar work, for groups of a
-// multiple of 8 queries; the tail block query-minor)
 __device__ __forceinline__ uint64_t job_id(const NfaArgs& A, uint64_t idx) {
   if (A.jobs) return A.jobs[idx];
   const uint32_t nq = A.n_q ? A.n_q : 1;
-  uint64_t rank = idx / nq;
-  uint32_t qi = (uint32_t)(idx % nq);
-  if (A.job_map == 1 && nq % 8 == 0) {
-    const uint64_t blk = idx / (64ull * nq);
-    if ((blk + 1) * 64 <= A.n_keys) {
-      const uint64_t in = idx % (64ull * nq), w = in / 64, l = in % 64, qo = nq / 8;
-      qi = (uint32_t)((w % qo) * 8 + l % 8);
-      rank = blk * 64 + (w / qo) * 8 + l / 8;
-    }
-  }
+  const uint64_t rank = idx / nq;
+  const uint32_t qi = (uint32_t)(idx % nq);
   return (uint64_t)qi * A.n_keys + (A.order ? A.order[rank] : rank);
 }
 
@@ -1940,31 +1529,26 @@ __device__ __forceinline__ void run_key(const NfaArgs& A, Q& q, v4u* lds = nullp
   }
 #endif
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // A lane without a job stays in its wave with no events (has false): the wave-wide loops and
-  // the coop pages' shuffles (nfa_coop.h) read every lane of the wave, so none may have left.
+  // A lane without a job stays in its wave with no events (has false): the wave-wide loops
+  // read every lane of the wave, so none may have left.
   bool has = true;
   uint64_t job = 0;
-  if (A.solo) {  // one job per wave, alone (session.cpp: beside the persistent launch)
-    has = slot % 64 == 0 && slot / 64 < A.n_jobs;
-    if (has) job = job_id(A, slot / 64);
-  } else if (A.jobs) {
+  if (A.jobs) {
     if (slot >= A.n_jobs) has = false;
     else job = A.jobs[slot];
   } else {
     const uint32_t nq = A.n_q ? A.n_q : 1;
     const uint64_t w = slot / 64;
     // spread: the heaviest W keys (lane order) lead one wave each, the next W are their lanes 1,
-    // ...; spread_snake: odd lanes take their row in reverse (wave 0's lane 1 is the row's
-    // lightest key), so the waves of the heaviest keys carry the lightest neighbours
+    // ...; odd lanes take their row in reverse (wave 0's lane 1 is the row's lightest key), so
+    // the waves of the heaviest keys carry the lightest neighbours
     const uint64_t l = slot % 64;
     uint64_t rank;
     if (A.spread && w >= A.spread) {  // (the grid's last block past the W waves: idle)
       rank = ~0ull;
-    } else if (A.spread && w < A.spread_iso) {  // a heavy rank alone in its wave: no divergent neighbours
-      rank = l == 0 ? w : ~0ull;
     } else if (A.spread) {
-      const uint64_t W = A.spread - A.spread_iso, w2 = w - A.spread_iso;
-      rank = A.spread_iso + l * W + ((A.spread_snake && (l & 1)) ? W - 1 - w2 : w2);
+      const uint64_t W = A.spread;
+      rank = l * W + ((l & 1) ? W - 1 - w : w);
     } else if (A.spread_iso && w < A.spread_iso) {  // (lane order) the heaviest ranks alone
       rank = l == 0 ? w : ~0ull;
     } else if (A.spread_iso) {

@@ -183,6 +183,8 @@ struct GroupRt {
   hipModule_t mod_stream = nullptr;  // streaming sessions: the stream build (jit_stream_source)
   hipFunction_t fn_stream = nullptr;
   uint32_t waves_cu = 0, waves_cu_wide = 0;  // resident waves per CU of fn / fn_wide (occupancy)
+  uint32_t waves_cu_stream = 0;               // ... of fn_stream (streams run it)
+  uint32_t walk_flush = 24;  // the drain threshold the group's kernels were compiled with
   hipFunction_t fn_est = nullptr;   // cep_nfa_est (begin stage = one BEGIN edge)
   hipFunction_t fn_bits = nullptr;  // cep_nfa_bits (the same queries): begin-hit bitmap
   double jit_compile_s = 0;
@@ -213,8 +215,6 @@ struct cep_session {
   cep::Tuning tune{};  // measurement knobs, read once at creation (tuning.cpp)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-  hipStream_t solo_stream = nullptr;  // kernel groups: the solo launch beside the main one
-  hipEvent_t solo_ev0 = nullptr, solo_ev1 = nullptr;
   int cus = 256;  // compute units of the device (persistent-lane grids)
   std::vector<std::unique_ptr<QueryRt>> qs;
   std::vector<std::unique_ptr<GroupRt>> groups;
@@ -303,12 +303,15 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint64_t n_groups = n_tiles / 64 + 2;
   s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));                          // tile counts
   s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
-  s->mask.ensure(sizeof(uint64_t) * 4 * (s->n_events / 256 + 2));  // 4 ballot words per 256 events
+  s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));                     // a match word per 64 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
   s->bnd.ensure(sizeof(uint32_t) * 2 * (s->n_events / 64 + 2));                   // word -> key, sequence number
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
-  if (!r.h_sc) HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocMapped));
+  if (!r.h_sc) {
+    HIPCHECK(hipHostMalloc((void**)&r.h_sc, sizeof(Scratch), hipHostMallocMapped));
+    std::memset(r.h_sc, 0, sizeof(Scratch));
+  }
   if (s->n_events == 0) {
     // launch_stencil launches nothing, so nothing writes this batch's count into the pinned
     // copy: zero it here, once an earlier batch's stencil_emit can no longer overwrite it
@@ -365,7 +368,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   HIPCHECK(launch_wave_keys(s->key_off, nk, s->n_events, s->keylist.as<uint32_t>(), reinterpret_cast<uint32_t*>(sc),
                             (uint32_t)((sizeof(Scratch) + sizeof(uint32_t) * n_groups) / 4), s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][1], s->stream));
-  HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->tune.stencil_pf, s->stream));
+  HIPCHECK(launch_stencil((int)m, a, range, q->nRangeCols, s->stream));
   HIPCHECK(hipEventRecord(r.tev[slot][2], s->stream));
   r.pending = true;
   r.launches = 2;  // stencil_mask + stencil_emit
@@ -419,7 +422,9 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // waves per CU of the JIT kernels (compile.cpp): the narrow build 3 per SIMD, the wide one
   // (streams, re-runs) 2; $CEP_RESIDENT_WAVES (per CU): measurement runs
   const uint64_t wn = g.waves_cu ? g.waves_cu : 12, ww = g.waves_cu_wide ? g.waves_cu_wide : 8;
-  uint64_t waves_cu = streaming ? ww : wn, waves_cu_wide = ww;
+  // (a stream runs the stream build when it has one: its own occupancy)
+  const uint64_t wst = g.fn_stream && g.waves_cu_stream ? g.waves_cu_stream : ww;
+  uint64_t waves_cu = streaming ? wst : wn, waves_cu_wide = ww;
   if (s->tune.resident_waves > 0) waves_cu = waves_cu_wide = s->tune.resident_waves;
   const uint64_t resident = (uint64_t)s->cus * waves_cu * 64;
   const uint64_t resident_wide = (uint64_t)s->cus * waves_cu_wide * 64;
@@ -436,45 +441,29 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // divergent lanes.  So its keys are spread over every wave slot the chip holds: the heaviest
   // keys lead one wave each, with lighter keys beside them ($CEP_SPREAD=0: measurement runs).
   uint64_t spread = 0;
-  // (odd lanes take their row of ranks reversed: the slowest world-8 shard 16.5 -> 15.6 ms;
-  // $CEP_SPREAD: 0 off, 1 rows in order, 2 (default) odd lanes reversed - measurement runs)
-  uint32_t snake = 0;
-  if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64) {
-    const int mode = s->tune.spread;
-    if (mode != 0) spread = std::min<uint64_t>(resident / 64, nk);
-    snake = mode == 2 ? 1u : 0u;
-  }
+  // (odd lanes take their row of ranks reversed: the slowest world-8 shard 16.5 -> 15.6 ms)
+  if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64 && !s->tune.no_spread)
+    spread = std::min<uint64_t>(resident / 64, nk);
   // (a full launch spread over all its waves - every wave led by one of the heaviest keys with
-  // lighter ones beside it - was measured: cfg 3 29.2 -> 48.8 ms, every wave pays the divergence)
-  // heavy ranks alone in their waves (measurement knob): only while the rest still fit
+  // lighter ones beside it - was measured: cfg 3 29.2 -> 48.8 ms, every wave pays the divergence;
+  // so was isolating a spread launch's heaviest ranks in waves of their own: the slowest world-8
+  // shard 15.4 -> 14.4-15.2 ms, within its spread - dropped in round 5)
   uint32_t iso = 0;
-  if (spread && s->tune.isolate) {
-    iso = (uint32_t)std::min<uint64_t>(s->tune.isolate, spread - 1);
-    while (iso > 0 && (uint64_t)iso + (spread - iso) * 64 < nk) iso /= 2;
-  }
   // A stream launch bigger than the chip: its K heaviest keys (by the lane order's estimate) run
   // alone in their waves, the others 64 per wave in lane order.  A streamed batch lasts as long as
   // its heaviest wave, and a heavy key's wave otherwise pays its lighter neighbours' divergent
-  // paths and drains too (streamed cfg 3, main launches: 61.3 -> 43.9 ms at K = 2048;
-  // $CEP_STREAM_ISO=K, 0 off: measurement runs)
-  // ($CEP_BATCH_ISO=K, measurement runs: the same for a per-batch launch)
-  if (!spread && !persist && Q == 1 && nk > 64) {
-    const uint32_t k = streaming ? s->tune.stream_iso : s->tune.batch_iso;
-    if (k) iso = (uint32_t)std::min<uint64_t>(k, nk / 2);
-  }
+  // paths and drains too (streamed cfg 3, main launches: 61.3 -> 43.9 ms at K = 2048).  (The same
+  // for a per-batch launch measured slower - 33.9 -> 36.9 ms at K = 2048: one launch of 1e9
+  // events is throughput-bound - and was dropped in round 5.)  Only with a lane order to pick the
+  // heaviest keys by (a begin stage with a single BEGIN edge has one): else the first keys by id
+  // would each take a wave for nothing.
+  const bool lane_order = g.fn_est && nk > 64 && !(streaming && s->tune.stream_no_order);
+  if (streaming && !spread && lane_order && s->tune.stream_iso)
+    iso = (uint32_t)std::min<uint64_t>(s->tune.stream_iso, nk / 2);
   const uint64_t slots = spread ? spread * 64
                          : iso  ? ((uint64_t)iso + (nk - iso + 63) / 64) * 64
                          : !persist ? ((nk + 63) / 64) * 64 * Q
                                     : grid_for(jobs);
-  // Solo jobs (kernel groups): the jobs of the `solo` heaviest keys by the lane order, each alone
-  // in a wave of its own, launched beside the persistent launch (which claims the rest).  A
-  // group's launch otherwise lasts as long as its heaviest jobs do in waves shared with other
-  // jobs' divergent paths and drains (config 5: the longest wave ~3x the mean); alone, a heavy job
-  // runs its own path only, and the light ones among them finish at once and free their slots.
-  // (at most 16384 solo jobs: each holds a 64-lane wave's run queues and walk queue)
-  const uint64_t solo_jobs =
-      (persist && g.fn_est && nk > 64) ? std::min<uint64_t>(std::min<uint64_t>((uint64_t)s->tune.solo_keys, nk / 4) * Q, 16384) : 0;
-  const uint64_t solo_slots = solo_jobs * 64;
   g.ks.ensure(sizeof(KeyState) * std::max<uint64_t>(jobs, 1));
   s->scratch.ensure(sizeof(Scratch));
   Scratch* sc = s->scratch.as<Scratch>();
@@ -506,18 +495,18 @@ void run_nfa(cep_session* s, GroupRt& g) {
   s->preds0.ensure(sizeof(Pred) * node_cap);
   s->preds.ensure(sizeof(Pred) * pred_cap);
   s->out.ensure(sizeof(uint32_t) * kOutChunkWords * out_cap);
-  s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap) + ring_size(g.F, solo_slots, rcap));
-  // deferred walks a key can queue (nfa_lane.h drains at the compiled CEP_WALK_FLUSH, the
-  // same value as tune.walk_flush; $CEP_WALK_CAP: tuning)
+  s->rings.ensure(ring_size(g.F, std::max<uint64_t>(slots, 1), rcap));
+  // deferred walks a key can queue (nfa_lane.h drains at the compiled CEP_WALK_FLUSH, recorded
+  // with the group; $CEP_WALK_CAP: tuning)
   // (a stream cannot re-run a key whose event overflows its queue: room for every walk one
   // event can queue - removePattern and branch walks of its records, one extraction per output
   // - beyond the drain threshold)
-  uint32_t wcap = streaming ? std::max<uint32_t>(64, s->tune.walk_flush + 3 * rcap) : 64;
+  uint32_t wcap = streaming ? std::max<uint32_t>(64, g.walk_flush + 3 * rcap) : 64;
   if (s->tune.walk_cap) wcap = s->tune.walk_cap;
   // put-log entries per lane: every put one event can log fits twice over (a stream turns a
   // put-log overflow into a sticky error, so it must never happen there)
   uint32_t plog = put_log_entries(rcap);
-  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap, plog) + walkq_size(solo_slots, wcap, plog));
+  s->walks.ensure(walkq_size(std::max<uint64_t>(slots, 1), wcap, plog));
   HIPCHECK(hipMemsetAsync(sc, 0, sizeof(Scratch), s->stream));
 
   NfaArgs a{};
@@ -574,7 +563,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   a.defer = 1;
   a.n_q = (uint32_t)Q;
   a.spread = spread;
-  a.spread_snake = snake;
   a.spread_iso = iso;
   a.kc = g.kc.bytes ? g.kc.as<int64_t>() : nullptr;
   a.nodes = s->nodes.as<Node>();
@@ -591,7 +579,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   if (persist) {
     a.job_next = &sc->job_next;
     a.n_jobs = jobs;
-    a.job_map = s->tune.job_map;  // (measurement runs)
   }
   if (streaming) {  // walks deferred too: a conflict resolves exactly without a re-run (nfa_lane.h)
     a.rings = S.rings.p;
@@ -651,25 +638,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // error - and $CEP_STREAM_NO_ORDER: without the lane order; measurement runs only)
   const bool stream_narrow = s->tune.stream_narrow;
   if (streaming && s->tune.stream_no_order) a.order = nullptr;
-  if (solo_jobs && a.order) {
-    // the solo launch first, on its own stream (after everything above on the session stream);
-    // the persistent lanes claim from the first job past the solo ones
-    NfaArgs b = a;
-    b.job_next = nullptr;
-    b.solo = 1;
-    b.n_jobs = solo_jobs;
-    b.rings = (char*)s->rings.p + ring_size(g.F, std::max<uint64_t>(slots, 1), rcap);
-    b.walks = (char*)s->walks.p + walkq_size(std::max<uint64_t>(slots, 1), wcap, plog);
-    HIPCHECK(hipEventRecord(s->solo_ev0, s->stream));
-    HIPCHECK(hipStreamWaitEvent(s->solo_stream, s->solo_ev0, 0));
-    HIPCHECK(launch_nfa_tier(g, r0.q, b, solo_slots, s->solo_stream, false));
-    HIPCHECK(hipEventRecord(s->solo_ev1, s->solo_stream));
-    HIPCHECK(hipMemsetD32Async((hipDeviceptr_t)&sc->job_next, (int)solo_jobs, 1, s->stream));
-    launches++;
-  }
   if (streaming && g.fn_stream) HIPCHECK(launch_fn(g.fn_stream, a, (slots + 255) / 256, s->stream));
   else HIPCHECK(launch_nfa_tier(g, r0.q, a, slots, s->stream, streaming && !stream_narrow));
-  if (solo_jobs && a.order) HIPCHECK(hipStreamWaitEvent(s->stream, s->solo_ev1, 0));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   launches++;
   Scratch h{};
@@ -792,7 +762,10 @@ void run_nfa(cep_session* s, GroupRt& g) {
     // (re-runs take the wide build: its occupancy; the interpreter tier keeps the default)
     auto grid_re = [&](uint64_t n) { return g.fn ? grid_wide(n) : grid_for(n); };
     const uint64_t most = grid_re(std::max<uint64_t>(lens[0], lens[1]));
-    while (rcap > 32 && most && ring_size(g.F, most, rcap) > (16ull << 30)) rcap /= 2;
+    // (the walk queues' put logs grow with rcap too: both within the cap)
+    while (rcap > 32 && most &&
+           ring_size(g.F, most, rcap) + walkq_size(most, wcap, put_log_entries(rcap)) > (16ull << 30))
+      rcap /= 2;
     a.rcap = rcap;
     s->retry_rings.ensure(ring_size(g.F, std::max<uint64_t>(most, 1), rcap));
     plog = put_log_entries(rcap);
@@ -923,10 +896,10 @@ int cep_jit_precompile(const cep_query* q, double* compile_s) {
   if (!q) return fail(CEP_E_INVALID, "null query");
   try {
     double w = 0;
-    jit_code_object(q->jitSource, compile_s);
-    jit_code_object(jit_wide_source(q->jitSource), &w);
+    jit_code_object(q->jitSource, compile_s, true);
+    jit_code_object(jit_wide_source(q->jitSource), &w, true);
     if (compile_s) *compile_s += w;
-    jit_code_object(jit_stream_source(q->jitSource), &w);  // (streaming sessions over the query)
+    jit_code_object(jit_stream_source(q->jitSource), &w, true);  // (streaming sessions over the query)
     if (compile_s) *compile_s += w;
   } catch (std::exception& e) {
     return fail(CEP_E_COMPILE, e.what());
@@ -945,8 +918,8 @@ int cep_jit_precompile_group(const cep_query* const* queries, int n_queries, dou
   try {
     for (auto& pl : plan_groups(qv)) {
       double t = 0, w = 0;
-      jit_code_object(pl.source, &t);
-      jit_code_object(jit_wide_source(pl.source), &w);
+      jit_code_object(pl.source, &t, true);
+      jit_code_object(jit_wide_source(pl.source), &w, true);
       if (compile_s) *compile_s += t + w;
     }
   } catch (std::exception& e) {
@@ -1012,9 +985,6 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
     HIPCHECK(hipEventCreate(&s->ev0));
     HIPCHECK(hipEventCreate(&s->ev1));
     HIPCHECK(hipEventCreate(&s->ev2));
-    HIPCHECK(hipStreamCreateWithFlags(&s->solo_stream, hipStreamNonBlocking));
-    HIPCHECK(hipEventCreateWithFlags(&s->solo_ev0, hipEventDisableTiming));
-    HIPCHECK(hipEventCreateWithFlags(&s->solo_ev1, hipEventDisableTiming));
     for (int i = 0; i < n_queries; i++) {
       auto r = std::make_unique<QueryRt>();
       r->q = queries[i];
@@ -1054,6 +1024,11 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         s->qs[pl.members[k]]->group = (int)s->groups.size();
         s->qs[pl.members[k]]->qi = (uint32_t)k;
       }
+      {  // (the source's CEP_WALK_FLUSH: the value its kernels drain at, whatever the session's
+         // environment says now - ADVICE r4)
+        const size_t at = pl.source.find("#define CEP_WALK_FLUSH ");
+        if (at != std::string::npos) g->walk_flush = (uint32_t)std::strtoul(pl.source.c_str() + at + 23, nullptr, 10);
+      }
       if (s->opts.tier == CEP_TIER_JIT) {  // the group's own kernel, compiled by hipRTC
         std::vector<char> co = jit_code_object(pl.source, &g->jit_compile_s);
         HIPCHECK(hipModuleLoadData(&g->mod, co.data()));
@@ -1079,6 +1054,10 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
         nb = 0;
         if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, g->fn_wide, 256, 0) == hipSuccess && nb > 0)
           g->waves_cu_wide = (uint32_t)nb * 4;
+        nb = 0;
+        if (g->fn_stream && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, g->fn_stream, 256, 0) == hipSuccess &&
+            nb > 0)
+          g->waves_cu_stream = (uint32_t)nb * 4;
         if (pl.source.find("cep_nfa_est") != std::string::npos) {  // (a failed lookup would stick)
           HIPCHECK(hipModuleGetFunction(&g->fn_est, g->mod, "cep_nfa_est"));
           HIPCHECK(hipModuleGetFunction(&g->fn_bits, g->mod, "cep_nfa_bits"));
@@ -1127,9 +1106,6 @@ void cep_session_destroy(cep_session* s) {
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->ev2) (void)hipEventDestroy(s->ev2);
-    if (s->solo_ev0) (void)hipEventDestroy(s->solo_ev0);
-    if (s->solo_ev1) (void)hipEventDestroy(s->solo_ev1);
-    if (s->solo_stream) (void)hipStreamDestroy(s->solo_stream);
     if (s->stream) (void)hipStreamDestroy(s->stream);
   }
   delete s;
@@ -1182,7 +1158,7 @@ static void partition_batch(cep_session* s, const cep_batch* b) {
   HIPCHECK(partition(keys, n, nk, (int)nf, in, out, wide, ts, ts ? s->p_ts.as<int64_t>() : nullptr,
                      s->p_off.as<uint64_t>(), s->p_cnt.as<uint64_t>(), s->p_perm.as<uint32_t>(),
                      s->p_sorted.as<uint32_t>(), s->p_idx.as<uint32_t>(), s->p_scratch.p, sb, &sc->overflow,
-                     s->stream, s->tune.part_rounds, s->tune.gather_per));
+                     s->stream, s->tune.part_rounds));
   HIPCHECK(hipEventRecord(s->ev1, s->stream));
   uint32_t bad = 0;
   HIPCHECK(hipMemcpyAsync(&bad, &sc->overflow, sizeof bad, hipMemcpyDeviceToHost, s->stream));

@@ -8,18 +8,20 @@
 // (proof: SURVEY Appendix A.5).  That is a 1-D stencil over the column:
 // HBM-bound, one pass.
 //
-// Layout.  A tile is 256 threads x 64 consecutive events; a thread reads its 64 int32 values
-// with sixteen 16-B loads (plus the m-1 halo events), evaluates the m stage predicates into
-// 64-bit masks and ANDs them shifted (match bit i = Π_x P_{m-1-x}(i-x)).  Key starts come
-// from a bitmap built once per batch, so a window crossing a key start is masked with
-// shifts, and a match's key is the tile's first key advanced by the key starts before it.
+// Layout.  A tile is 4 waves x 4096 consecutive events.  A wave streams its events with 16-B
+// loads (lane l holds events 4l..4l+3 of a 256-event step), evaluates the m stage predicates
+// straight into scalar ballot words and ANDs them shifted (match bit i = Π_x P_{m-1-x}(i-x));
+// the windows reaching back before the wave and those crossing a key start are settled after
+// the loop on natural 64-event words (key starts from key_off around the wave's first key,
+// wave_keys), and a match's key is its word's first key advanced over the key starts.
 //
-// Passes.  (1) stencil_mask streams the column once (a wave issues all its loads before the
-// first is used) and writes one 64-bit match mask per 64 events (1 bit/event) and a count per
-// tile; (2) stencil_emit sums the counts of the tiles before its own, reads the masks back
-// (1/32 of the column's bytes) and writes the matches in order.  No tile waits on another, so the streaming pass runs at HBM rate (a single-pass
-// decoupled look-back was measured latency-bound here: rounds of co-resident tiles look back
-// through each other).
+// Passes.  (1) stencil_mask streams the column once and writes one 64-bit match word per 64
+// events (1 bit/event), the word's key and sequence number, and a count per tile; (2)
+// stencil_emit sums the counts of the tiles before its own, reads the words back (1/32 of the
+// column's bytes) and writes the matches in order.  No tile waits on another.  (A single pass
+// with a decoupled look-back over the tile counts was measured slower: 126.7 us against 112.6
+// for the two passes at round 5's start, profiles/r05/ - a tile waits for every tile before
+// it, ~24 look-back round trips deep within one round of co-resident tiles.)
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -87,14 +89,21 @@ __device__ __forceinline__ uint64_t mix64s(uint64_t z) {
 
 __device__ __forceinline__ bool in_range(int64_t v, int64_t lo, int64_t hi) { return v >= lo && v <= hi; }
 
+// bit m of a 16-bit value -> bit 4 m
+__device__ __forceinline__ uint64_t spread4(uint32_t x16) {
+  uint64_t x = x16;
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+
 // Pass 1 layout.  A wave owns kStWave consecutive events and reads them with 16-B loads in
 // which lane l holds events 4l..4l+3 of a 256-event step: every load instruction covers
-// 1 KiB contiguous (fully coalesced).  Per step a lane evaluates the M stage predicates
-// into 4-bit nibbles; the window needs the M-1 <= 7 events before the nibble, i.e. the
-// nibbles of lanes l-1 and l-2 (cross-lane shuffles) or, for lanes 0-1, of lanes 62-63 of
-// the previous step (wave-uniform carries).  Key starts come the same way from the bitmap.
+// 1 KiB contiguous (fully coalesced).  Per step the M stage predicates go straight into scalar
+// ballot words and the windows are ANDs of shifted words (stage s sits M-1-s events back).
 constexpr int kStSteps = kStWave / 256;               // 16 load steps per wave
-constexpr int kStDefaultPF = 1;
 
 template <int M, bool RANGE, int NCOL>
 struct StEval {
@@ -131,16 +140,8 @@ struct StEval {
       P[s] |= (ok ? 1u : 0u) << bit;
     }
   }
-  // stage s over one event per lane, straight into a ballot word: each compare's own lane
-  // mask (llvm.amdgcn.ballot of a compare is the v_cmp result), ANDed in scalar registers
-  __device__ __forceinline__ uint64_t ballot(int s, int32_t x0, int32_t x1) const {
-    uint64_t m = __builtin_amdgcn_ballot_w64(x0 >= lo[s][0]) & __builtin_amdgcn_ballot_w64(x0 <= hi[s][0]);
-    if (NCOL > 1) m &= __builtin_amdgcn_ballot_w64(x1 >= lo[s][1]) & __builtin_amdgcn_ballot_w64(x1 <= hi[s][1]);
-    return m;
-  }
   // stage s over the 4 events of a step: W[k] = ballot word of event 4 l + k.  Every
-  // operation is a vector op whose result lands in scalar registers (the compare mask);
-  // the scalar unit, shared by the CU's four SIMDs, is this kernel's tightest resource.
+  // operation is a vector op whose result lands in scalar registers (the compare mask)
   __device__ __forceinline__ bool in1(int s, int c, int32_t v) const {
     return (uint32_t)v - (uint32_t)lo[s][c] <= span[s][c];
   }
@@ -172,50 +173,54 @@ struct StEval {
   }
 };
 
-template <int M, bool RANGE, int NCOL, int PF>
-__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
-  static_assert(kStSteps % PF == 0, "prefetch depth divides the wave's steps");
+// What the mask phase leaves a wave (kStWave events from wbase), per lane, for its natural
+// 64-event word (events ws .. ws + 63, ws = wbase + 64 lane):
+struct WaveMask {
+  uint64_t nat;   // bit i: a match (a window of M events of one key) ends at event ws + i
+  uint64_t bw;    // bit i: a key starts at event ws + i
+  uint32_t wkey;  // the key holding event ws (the largest key whose offset is <= ws)
+  uint64_t wks;   // that key's first event
+};
+
+// The mask phase of one wave.  The steps' loads are double-buffered (one step in flight while
+// the other computes) and the step loop carries nothing but the stage words of the previous
+// step: the windows that reach back before the wave (the first M-1 ending in it) and the
+// windows crossing a key start are settled after the loop, on the natural words, with vector
+// work.  (This keeps the loop's scalar registers down - 58 instead of 106, 8 waves per SIMD
+// instead of 6 - and the pass at ~75 us for 1e8 events instead of ~90: profiles/r05/.)
+template <int M, bool RANGE, int NCOL>
+__device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t wbase, const int lane, WaveMask& out) {
   constexpr int H = M - 1;              // events a window reaches back
-  __shared__ uint32_t s_cnt[kStThreads / 64];
-  // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
-  // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
   const StEval<M, RANGE, NCOL> ev(A);
   const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never;
-  // The fast path's first PF steps are requested before anything else: the key-start words
-  // and the seed events below are dependent round trips, and a wave only lives 16 steps.
+  // The fast path's first step is requested before anything else: the key-start words and
+  // the seed events below are dependent round trips
   const v4i* c0 = reinterpret_cast<const v4i*>(A.col[0] + wbase) + lane;
   const v4i* c1 = reinterpret_cast<const v4i*>(A.col[NCOL - 1] + wbase) + lane;
-  v4i xb[PF], yb[PF];
-#pragma unroll
-  for (int d = 0; d < PF; d++) xb[d] = yb[d] = v4i{0, 0, 0, 0};
+  v4i xa = {0, 0, 0, 0}, ya = {0, 0, 0, 0};
   if (fast) {
-#pragma unroll
-    for (int d = 0; d < PF; d++) {
-      xb[d] = __builtin_nontemporal_load(c0 + d * 64);
-      yb[d] = NCOL > 1 ? __builtin_nontemporal_load(c1 + d * 64) : xb[d];
-    }
+    xa = __builtin_nontemporal_load(c0);
+    ya = NCOL > 1 ? __builtin_nontemporal_load(c1) : xa;
   }
-  // the key holding the wave's first event (wave_keys); the seed loads below go out with it
+  // the key holding the wave's first event (wave_keys)
   const uint64_t n_waves = (A.n_events + kStWave - 1) / kStWave;  // n_events >= 1: the tile exists
   const uint64_t wi = wbase / kStWave;
   const uint32_t k0 = A.wave_key[wi < n_waves ? wi : n_waves - 1];
-  // the 8 events before the wave (lanes 0..7; the others load the same lines)
-  const uint64_t sp0 = (wbase >= 8 ? wbase - 8 : 0) + (uint64_t)(lane & 7);
-  const uint64_t sp = sp0 < A.n_events ? sp0 : A.n_events - 1;
+  // the seed events wbase - H .. wbase + H - 1 (lane j < 2H: event wbase - H + j): the windows
+  // ending at the wave's first H events, settled after the loop
+  const int64_t sp = (int64_t)wbase - H + lane;
+  const bool sv = H > 0 && lane < 2 * H && sp >= 0 && (uint64_t)sp < A.n_events;
   int32_t sx0 = 0, sx1 = 0;
-  if (RANGE && H > 0) {
+  if (RANGE && sv) {
     sx0 = A.col[0][sp];
     sx1 = A.col[NCOL - 1][sp];
   }
-  if (RANGE && H > 0) asm volatile("" ::"v"(sx0), "v"(sx1));  // keeps the seed loads up here
   // Key starts in [wbase - 8, wend): lanes read key_off[k0 - 8 + 64 c + lane] (the 8 keys
   // before k0 may start among the 8 events before the wave) and a wave-uniform loop visits
-  // the starts in range, in key order.  bw: this lane's start bits (events wbase + 64 lane
-  // ..+63), pkb: starts among the 8 events before the wave (bit x: event wbase - 8 + x),
-  // wkey: the key holding event wbase + 64 lane (for stencil_emit: the largest key whose
-  // offset is <= it; empty keys share their successor's offset and lose to it).
+  // the starts in range, in key order.  bw: this lane's start bits, pkb: starts among the 8
+  // events before the wave (bit x: event wbase - 8 + x), wkey: the key holding event ws (for
+  // stencil_emit: the largest key whose offset is <= it; empty keys share their successor's
+  // offset and lose to it).
   const uint64_t wend = wbase + kStWave < A.n_events ? wbase + kStWave : A.n_events;
   const uint64_t lo = wbase >= 8 ? wbase - 8 : 0;
   const uint64_t ws = wbase + (uint64_t)lane * 64;
@@ -251,39 +256,21 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
       if (!(i0 + 64 < (int64_t)A.n_keys && s63 < wend)) break;  // no key after this chunk starts in range
     }
   }
-  // steps with a key start (bit 4q + x: word x of step q is non-zero), mostly none
-  const uint64_t kstep = H > 0 ? __ballot(bw != 0) : 0;
-  // Ballot words of the previous step: bit l of W[s][k] = stage s holds at event 4l + k.
-  // Only their top two bits are read (events 4*62+k, 4*63+k): seed them with the 8 events
-  // before the wave.
-  uint64_t pW[M][4], pK[4];
-  {
-    uint32_t P[M];
+  // Ballot words of the previous step (bit l of W[s][k] = stage s holds at event 4l + k),
+  // zero before the wave's first step: windows reaching back before the wave are settled
+  // below from the seed events
+  uint64_t pW[M][4];
 #pragma unroll
-    for (int s = 0; s < M; s++) P[s] = 0;
-    if (H > 0 && lane < 8 && wbase >= (uint64_t)(8 - lane)) {
-      if (RANGE && sp0 < A.n_events) ev.range(sx0, sx1, P, 0);
-      else if (!RANGE) ev.one(A, wbase - 8 + lane, P, 0);
-    }
+  for (int s = 0; s < M; s++)
 #pragma unroll
-    for (int s = 0; s < M; s++) {
-      const uint64_t b = __ballot(P[s] & 1u);  // bit x: event wbase - 8 + x
-#pragma unroll
-      for (int k = 0; k < 4; k++) pW[s][k] = (((b >> k) & 1ull) << 62) | (((b >> (4 + k)) & 1ull) << 63);
-    }
-    const uint32_t pb = (H > 0 && wbase >= 8) ? pkb : 0u;
-#pragma unroll
-    for (int k = 0; k < 4; k++) pK[k] = (((uint64_t)(pb >> k) & 1ull) << 62) | (((uint64_t)(pb >> (4 + k)) & 1ull) << 63);
-  }
-  bool pk_any = ((pK[0] | pK[1] | pK[2] | pK[3]) >> 62) != 0;
-  uint64_t myword = 0;  // mask word wbase / 64 + lane = word k of step q for lane 4q + k
+    for (int k = 0; k < 4; k++) pW[s][k] = 0;
+  uint64_t myword = 0;  // ballot layout: word k of step q for lane 4q + k
   // step q of the wave: x/y hold its 4 events per lane on the fast path (FAST: a
   // std::integral_constant, so each loop below gets its own straight-line body)
   auto step = [&](const int q, const v4i x, const v4i y, auto fast_c) {
     constexpr bool FAST = decltype(fast_c)::value;
     const uint64_t e0 = wbase + (uint64_t)q * 256 + (uint64_t)lane * 4;
-    // stage words of this step (wave-uniform, scalar registers): bit l of W[s][k] = stage s
-    // holds at event 4l + k
+    // stage words of this step (wave-uniform, scalar registers)
     uint64_t W[M][4];
     if (FAST) {
 #pragma unroll
@@ -324,34 +311,6 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
         m[k] &= cr == 0 ? W[s][kk] : ((W[s][kk] << cr) | (pW[s][kk] >> (64 - cr)));
       }
     }
-    // A key start at any of the window's last M-1 events (offsets 0 .. M-2) kills it: only
-    // in steps holding a key start or right after one (a wave-uniform branch, rarely taken)
-    if (H > 0 && (((kstep >> (4 * q)) & 0xF) || pk_any)) {
-      uint64_t K[4] = {0, 0, 0, 0};
-      if ((kstep >> (4 * q)) & 0xF) {
-        // this lane's 4 key-start bits: word 4q + lane/16 of the wave (lanes 4q..4q+3 hold
-        // them), nibble lane % 16
-        const uint64_t b0 = __shfl(bw, 4 * q, 64), b1 = __shfl(bw, 4 * q + 1, 64);
-        const uint64_t b2 = __shfl(bw, 4 * q + 2, 64), b3 = __shfl(bw, 4 * q + 3, 64);
-        const int g = lane >> 4;
-        const uint64_t bword = g == 0 ? b0 : g == 1 ? b1 : g == 2 ? b2 : b3;
-        const uint32_t B = (uint32_t)(bword >> (4 * (lane & 15))) & 0xF;
-#pragma unroll
-        for (int k = 0; k < 4; k++) K[k] = __builtin_amdgcn_ballot_w64((B >> k) & 1u);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int o = 0; o < H; o++) {
-          const int t = k - o;
-          const int cr = t >= 0 ? 0 : (3 - t) / 4;
-          const int kk = t + 4 * cr;
-          m[k] &= ~(cr == 0 ? K[kk] : ((K[kk] << cr) | (pK[kk] >> (64 - cr))));
-        }
-#pragma unroll
-      for (int k = 0; k < 4; k++) pK[k] = K[k];
-      pk_any = ((K[0] | K[1] | K[2] | K[3]) >> 62) != 0;  // only the top two bits carry
-    }
     // lane 4q + k keeps word k (vector compare + select: no scalar work)
     const int lrel = lane - 4 * q;
 #pragma unroll
@@ -363,43 +322,91 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
       for (int s = 0; s < M; s++) pW[s][k] = W[s][k];
   };
   if (fast) {
-    // PF steps per chunk; the next chunk's PF loads are issued before this chunk's steps
-    // run.  The loads are unconditional (the last chunk re-reads itself): a load under a
-    // branch makes the waitcnt pass drain every outstanding load (vmcnt(0)) before the
-    // first use, which serialises the wave on HBM latency.
+    // two one-step buffers: while one step computes, the other's load is in flight.  The
+    // loads are unconditional (the last pair re-reads its own step): a load under a branch
+    // makes the waitcnt pass drain every outstanding load before the first use.
+    v4i xb, yb;
 #pragma unroll 1
-    for (int c = 0; c < kStSteps; c += PF) {
-      const int cn = c + PF < kStSteps ? c + PF : c;
-      v4i xn[PF], yn[PF];
-#pragma unroll
-      for (int d = 0; d < PF; d++) {
-        xn[d] = __builtin_nontemporal_load(c0 + (cn + d) * 64);
-        yn[d] = NCOL > 1 ? __builtin_nontemporal_load(c1 + (cn + d) * 64) : xn[d];
-      }
-#pragma unroll
-      for (int d = 0; d < PF; d++) step(c + d, xb[d], yb[d], std::true_type{});
-#pragma unroll
-      for (int d = 0; d < PF; d++) {
-        xb[d] = xn[d];
-        yb[d] = yn[d];
-      }
+    for (int q = 0; q < kStSteps; q += 2) {
+      xb = __builtin_nontemporal_load(c0 + (q + 1) * 64);
+      yb = NCOL > 1 ? __builtin_nontemporal_load(c1 + (q + 1) * 64) : xb;
+      step(q, xa, ya, std::true_type{});
+      const int qn = q + 2 < kStSteps ? q + 2 : q;
+      xa = __builtin_nontemporal_load(c0 + qn * 64);
+      ya = NCOL > 1 ? __builtin_nontemporal_load(c1 + qn * 64) : xa;
+      step(q + 1, xb, yb, std::true_type{});
     }
   } else {
     const v4i z = {0, 0, 0, 0};
     for (int q = 0; q < kStSteps; q++) step(q, z, z, std::false_type{});
   }
-  // one 512-B store: words 4q..4q+3 belong to step q (written when the step has an event)
-  if (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) A.mask[wbase / 64 + lane] = myword;
+  // natural words: events wbase + 256 q + 64 r + i (q = lane / 4, r = lane % 4) are bits
+  // 16 r .. 16 r + 15 of the ballot words of step q, held by lanes 4q .. 4q + 3
+  uint64_t nat = 0;
+  {
+    const int q4 = lane & ~3, r16 = 16 * (lane & 3);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint64_t wk = __shfl(myword, q4 + k, 64);
+      nat |= spread4((uint32_t)(wk >> r16) & 0xFFFFu) << k;
+    }
+  }
+  if (H > 0) {
+    // the windows ending at events wbase + i, i < H (they reach back before the wave): stage
+    // bits of the seed events, bit j of S[s] = stage s holds at event wbase - H + j; the window
+    // ending at wbase + i holds iff bit i + s of S[s] is set for every s
+    uint32_t P[M];
+#pragma unroll
+    for (int s = 0; s < M; s++) P[s] = 0;
+    if (sv) {
+      if (RANGE) ev.range(sx0, sx1, P, 0);
+      else ev.one(A, (uint64_t)sp, P, 0);
+    }
+    uint64_t seed = wbase >= (uint64_t)H ? (1ull << H) - 1ull : 0ull;
+#pragma unroll
+    for (int s = 0; s < M; s++) seed &= __ballot(P[s] & 1u) >> s;
+    if (lane == 0) nat |= seed;
+    // a key start at any of a window's last M-1 events (offsets 0 .. M-2) kills it: the start
+    // bits spread over the H events after them, carried across words (lane 0: the starts among
+    // the 8 events before the wave)
+    // (the shuffle outside the select: a permute reading an inactive lane returns 0)
+    const uint64_t up = __shfl_up(bw, 1, 64);
+    const uint64_t pw = lane == 0 ? (uint64_t)pkb << 56 : up;
+    uint64_t kill = bw;
+#pragma unroll
+    for (int o = 1; o < H; o++) kill |= (bw << o) | (pw >> (64 - o));
+    nat &= ~kill;
+  }
+  if (ws >= A.n_events) nat = 0;  // (the seed bits of a wave past the end)
+  out.nat = nat;
+  out.bw = bw;
+  out.wkey = wkey;
+  out.wks = wks;
+}
+
+// Pass 1: per wave the mask phase, its natural words, their keys and sequence numbers, and
+// the match count per tile (and per 64 tiles, for stencil_emit's offsets)
+template <int M, bool RANGE, int NCOL>
+__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
+  __shared__ uint32_t s_cnt[kStThreads / 64];
+  // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
+  // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
+  WaveMask o;
+  wave_mask<M, RANGE, NCOL>(A, wbase, lane, o);
+  const uint64_t ws = wbase + (uint64_t)lane * 64;
   // (bit 31: a key starts inside the word after its first event - stencil_emit walks key_off
   // there; elsewhere a match's sequence number is word_seq + its offset in the word)
   if (ws < A.n_events) {
-    A.word_key[wbase / 64 + lane] = wkey | ((bw & ~1ull) ? 0x80000000u : 0u);
-    A.word_seq[wbase / 64 + lane] = (uint32_t)(ws - wks);
+    A.mask[ws / 64] = o.nat;
+    A.word_key[ws / 64] = o.wkey | ((o.bw & ~1ull) ? 0x80000000u : 0u);
+    A.word_seq[ws / 64] = (uint32_t)(ws - o.wks);
   }
   // matches of the wave: popcount of each lane's word, summed over the wave once
-  uint32_t cnt = (wbase + (uint64_t)(lane >> 2) * 256 < A.n_events) ? (uint32_t)__popcll(myword) : 0u;
+  uint32_t cnt = (uint32_t)__popcll(o.nat);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
   if (lane == 0) s_cnt[wv] = cnt;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -409,19 +416,9 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   }
 }
 
-// bit m of a 16-bit value -> bit 4 m
-__device__ __forceinline__ uint64_t spread4(uint32_t x16) {
-  uint64_t x = x16;
-  x = (x | (x << 24)) & 0x000000FF000000FFull;
-  x = (x | (x << 12)) & 0x000F000F000F000Full;
-  x = (x | (x << 6)) & 0x0303030303030303ull;
-  x = (x | (x << 3)) & 0x1111111111111111ull;
-  return x;
-}
-
-// Pass 2: a thread per 64 events (a quarter of a step's ballot words), the tile's offset
-// from the group and tile counts, a block scan for the threads' offsets.  A match's key is
-// the thread's first key (word_key) advanced over the key offsets it passes.
+// Pass 2: a thread per 64-event word, the tile's offset from the group and tile counts, a
+// block scan for the threads' offsets.  A match's key is the thread's first key (word_key)
+// advanced over the key offsets it passes.
 template <int M>
 __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   // a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
@@ -433,24 +430,15 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const uint64_t t = blockIdx.x;
   const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
   // Every independent load is issued before the first use (addresses clamped, no branches):
-  // the step (256 events) holding this thread's 64 - 16 lanes of each of its 4 ballot words -
-  // its first key, and the counts of the tiles before it.
+  // this thread's word, its first key, and the counts of the tiles before it.
   const bool valid = p0 < A.n_events;
   const uint64_t pc = valid ? p0 : t * kStTile;  // a tile's first event always exists
-  const uint64_t* w = A.mask + (pc / 256) * 4;
-  const uint64_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const uint64_t w0 = A.mask[pc / 64];
   const uint32_t wk = A.word_key[pc / 64], seq0 = A.word_seq[pc / 64];
   uint32_t key = wk & 0x7FFFFFFFu;
   const bool cross = (wk >> 31) != 0;  // a key starts inside this thread's 64 events
-  uint32_t ck[4] = {0, 0, 0, 0};
-  if (valid) {
-    const int sh = 16 * (int)((p0 / 64) & 3);
-    ck[0] = (uint32_t)(w0 >> sh) & 0xFFFFu;
-    ck[1] = (uint32_t)(w1 >> sh) & 0xFFFFu;
-    ck[2] = (uint32_t)(w2 >> sh) & 0xFFFFu;
-    ck[3] = (uint32_t)(w3 >> sh) & 0xFFFFu;
-  }
-  const uint32_t cnt = __popc(ck[0]) + __popc(ck[1]) + __popc(ck[2]) + __popc(ck[3]);
+  uint64_t match = valid ? w0 : 0ull;
+  const uint32_t cnt = (uint32_t)__popcll(match);
   uint64_t kstart = 0, knext = 0;
   if (cnt && cross) {
     kstart = A.key_off[key];
@@ -488,8 +476,6 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const bool staged = tile_total <= kStage;  // block-uniform
   uint64_t o = toff + excl;
   uint32_t so = excl;  // slot within the tile
-  // natural order: event p0 + 4 l + k is bit l of ck[k] -> bit 4 l + k
-  uint64_t match = spread4(ck[0]) | (spread4(ck[1]) << 1) | (spread4(ck[2]) << 2) | (spread4(ck[3]) << 3);
   while (match) {
     const int i = __builtin_ctzll(match);
     match &= match - 1;
@@ -547,38 +533,31 @@ hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n
 uint64_t stencil_waves(uint64_t n_events) { return (n_events + kStWave - 1) / kStWave; }
 
 template <int M, bool RANGE, int NCOL>
-static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, int pf0, hipStream_t st) {
-  const dim3 g((uint32_t)n_tiles), b(kStThreads);
-  // prefetch depth of stencil_mask's fast path (steps of 256 events whose loads run ahead;
-  // the session's $CEP_STENCIL_PF knob, else kStDefaultPF); only the range fast path streams
-  // vector loads
-  const int pf = RANGE ? (pf0 == 1 || pf0 == 2 || pf0 == 4 ? pf0 : kStDefaultPF) : 1;
-  if (pf == 4) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 4 : 1>), g, b, 0, st, a);
-  else if (pf == 2) hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, RANGE ? 2 : 1>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, 1>), g, b, 0, st, a);
+static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
+  hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }
 
 template <int M>
-static hipError_t launch_m(const StencilArgs& a, bool range, int ncol, uint64_t n_tiles, int pf, hipStream_t st) {
-  if (range && ncol == 1) return launch_one<M, true, 1>(a, n_tiles, pf, st);
-  if (range) return launch_one<M, true, 2>(a, n_tiles, pf, st);
-  return launch_one<M, false, 1>(a, n_tiles, pf, st);
+static hipError_t launch_m(const StencilArgs& a, bool range, int ncol, uint64_t n_tiles, hipStream_t st) {
+  if (range && ncol == 1) return launch_one<M, true, 1>(a, n_tiles, st);
+  if (range) return launch_one<M, true, 2>(a, n_tiles, st);
+  return launch_one<M, false, 1>(a, n_tiles, st);
 }
 
-hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, int pf, hipStream_t st) {
+hipError_t launch_stencil(int m, const StencilArgs& a, bool range, int ncol, hipStream_t st) {
   const uint64_t n_tiles = (a.n_events + kStTile - 1) / kStTile;
   if (n_tiles == 0) return hipSuccess;
   switch (m) {
-    case 1: return launch_m<1>(a, range, ncol, n_tiles, pf, st);
-    case 2: return launch_m<2>(a, range, ncol, n_tiles, pf, st);
-    case 3: return launch_m<3>(a, range, ncol, n_tiles, pf, st);
-    case 4: return launch_m<4>(a, range, ncol, n_tiles, pf, st);
-    case 5: return launch_m<5>(a, range, ncol, n_tiles, pf, st);
-    case 6: return launch_m<6>(a, range, ncol, n_tiles, pf, st);
-    case 7: return launch_m<7>(a, range, ncol, n_tiles, pf, st);
-    case 8: return launch_m<8>(a, range, ncol, n_tiles, pf, st);
+    case 1: return launch_m<1>(a, range, ncol, n_tiles, st);
+    case 2: return launch_m<2>(a, range, ncol, n_tiles, st);
+    case 3: return launch_m<3>(a, range, ncol, n_tiles, st);
+    case 4: return launch_m<4>(a, range, ncol, n_tiles, st);
+    case 5: return launch_m<5>(a, range, ncol, n_tiles, st);
+    case 6: return launch_m<6>(a, range, ncol, n_tiles, st);
+    case 7: return launch_m<7>(a, range, ncol, n_tiles, st);
+    case 8: return launch_m<8>(a, range, ncol, n_tiles, st);
   }
   return hipErrorInvalidValue;
 }

@@ -24,7 +24,7 @@ struct StencilArgs {
   uint16_t stage_name[kMaxStencil];    // walk order: stage name of pair t (t = 0 is the final event)
   bool aligned;              // col[] 16-B aligned: vector loads
   // pass 1 -> pass 3
-  uint64_t* mask;            // per 256 events 4 words: bit l of word k = a match ends at event 4 l + k
+  uint64_t* mask;            // per 64 events a word: bit i = a match ends at event 64 w + i
   uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1); bit 31: a key
                              // starts inside the word after its first event
   uint32_t* word_seq;        // event 64 w's sequence number within that key (pass 1)

@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcep.so")
+# $CEP_MEASURE set: the measurement build (libcep_measure.so, Makefile `measure`), the one that
+# reads the $CEP_* tuning knobs; the release libcep.so runs the defaults
+LIB_PATH = os.path.join(_HERE, "libcep_measure.so" if os.environ.get("CEP_MEASURE") else "libcep.so")
 SYNTH_LIB_PATH = os.path.join(_HERE, "libcep_synth.so")  # bench/test generators (include/cep_synth.h)
 
 CEP_MEM_HOST, CEP_MEM_DEVICE = 0, 1

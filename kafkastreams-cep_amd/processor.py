@@ -47,8 +47,9 @@ record); the results forwarded are the same.  The store is whatever
 persistent store), or the `store` argument.  The blob is a versioned plain encoding (no
 pickle): the device snapshot's own binary format, then a JSON document of the retained records
 whose keys and values go through `key_serde` / `value_serde` (Kafka-style serdes:
-`serialize(obj) -> bytes`, `deserialize(bytes) -> obj`; the default is JSON, for keys and
-values that are JSON data - the README's StockEvent dicts, strings, numbers).
+`serialize(obj) -> bytes`, `deserialize(bytes) -> obj`; the default, `JsonSerde`, is JSON that
+keeps tuples, non-string dict keys, bytes and numpy scalars exact; process() checks the first
+record of every key against the serdes, so an unsupported type fails at once).
 
 There is no CPU matching path: without libcep.so and a GPU, `init()` raises.
 """
@@ -101,21 +102,67 @@ _CKPT_VERSION = 2
 
 
 class JsonSerde:
-    """The default key/value serde of the processor's checkpoint: JSON data (dicts, lists,
-    strings, numbers, booleans, None).  Anything else needs a serde of its own (the reference's
-    Kryo serde likewise accepts only registered classes, serde/KryoSerDe.java)."""
+    """The default key/value serde of the processor's checkpoint: JSON with the Python types a
+    key or a record value usually is kept exact - dicts (any hashable keys), lists, tuples,
+    strings, numbers (non-finite floats too), booleans, None, bytes and numpy scalars; a tuple key
+    comes back a tuple, a dict value with int keys comes back with int keys.  Anything else (an
+    object read by attribute, say) needs a serde of its own: process() checks the first record of
+    every key against the serdes, so such a value fails there, not at the first commit (the
+    reference's Kryo serde likewise accepts only registered classes, serde/KryoSerDe.java)."""
 
-    @staticmethod
-    def serialize(obj) -> bytes:
-        try:
-            return json.dumps(obj, separators=(",", ":"), allow_nan=False).encode()
-        except (TypeError, ValueError) as e:
-            raise TypeError(f"cannot checkpoint {type(obj).__name__} values as JSON: pass key_serde/"
-                            f"value_serde to CEPProcessor") from e
+    TAG = "__cep__"  # a dict holding this key is an encoded non-JSON value
 
-    @staticmethod
-    def deserialize(data: bytes):
-        return json.loads(data.decode())
+    @classmethod
+    def _enc(cls, o):
+        if isinstance(o, (np.integer, np.floating, np.bool_)):  # (before float: np.float64 is one)
+            return {cls.TAG: "np", "dt": o.dtype.str, "v": cls._enc(o.item())}
+        if o is None or isinstance(o, (bool, str)):
+            return o
+        if isinstance(o, int):
+            return int(o)
+        if isinstance(o, float):
+            return o if o == o and o not in (float("inf"), float("-inf")) else {cls.TAG: "float", "v": repr(o)}
+        if isinstance(o, list):
+            return [cls._enc(x) for x in o]
+        if isinstance(o, tuple):
+            return {cls.TAG: "tuple", "v": [cls._enc(x) for x in o]}
+        if isinstance(o, dict):
+            if cls.TAG not in o and all(isinstance(k, str) for k in o):
+                return {k: cls._enc(v) for k, v in o.items()}
+            return {cls.TAG: "dict", "v": [[cls._enc(k), cls._enc(v)] for k, v in o.items()]}
+        if isinstance(o, (bytes, bytearray)):
+            return {cls.TAG: "bytes", "v": base64.b64encode(bytes(o)).decode()}
+        raise TypeError(f"cannot checkpoint {type(o).__name__} values as JSON: pass key_serde/value_serde "
+                        f"to CEPProcessor")
+
+    @classmethod
+    def _dec(cls, o):
+        if isinstance(o, list):
+            return [cls._dec(x) for x in o]
+        if not isinstance(o, dict):
+            return o
+        tag = o.get(cls.TAG)
+        if tag is None:
+            return {k: cls._dec(v) for k, v in o.items()}
+        if tag == "tuple":
+            return tuple(cls._dec(x) for x in o["v"])
+        if tag == "dict":
+            return {cls._dec(k): cls._dec(v) for k, v in o["v"]}
+        if tag == "float":
+            return float(o["v"])
+        if tag == "bytes":
+            return base64.b64decode(o["v"])
+        if tag == "np":
+            return np.dtype(o["dt"]).type(cls._dec(o["v"]))
+        raise ValueError(f"unknown checkpoint value tag {tag!r}")
+
+    @classmethod
+    def serialize(cls, obj) -> bytes:
+        return json.dumps(cls._enc(obj), separators=(",", ":"), allow_nan=False).encode()
+
+    @classmethod
+    def deserialize(cls, data: bytes):
+        return cls._dec(json.loads(data.decode()))
 
 
 # ---- Event / Sequence ---------------------------------------------------------------------
@@ -367,6 +414,9 @@ class CEPProcessor:
         if kid is None:
             if len(self._keys) >= self.max_keys:
                 raise ValueError(f"more than max_keys={self.max_keys} distinct keys")
+            if not self.in_memory:  # the checkpoint must hold this key and its records
+                self._check_serde(self.key_serde, key, "key")
+                self._check_serde(self.value_serde, value, "value")
             kid = self._key_ids[key] = len(self._keys)
             self._keys.append(key)
             self._events.append([])
@@ -381,6 +431,26 @@ class CEPProcessor:
         self._buf_ts.append(ev.timestamp)
         if len(self._buf_key) >= self.batch_size:
             self.flush()
+
+    @staticmethod
+    def _check_serde(serde, obj, what) -> None:
+        """A key (and the first record value of each key) must survive the checkpoint's serde:
+        an unsupported type fails at its first record, not at the next commit.  A key must also
+        come back equal and hashable (restore() indexes the keys)."""
+        try:
+            back = serde.deserialize(serde.serialize(obj))
+        except Exception as e:
+            raise TypeError(f"CEPProcessor checkpoint: the record {what} {obj!r} does not go through "
+                            f"{getattr(serde, '__name__', type(serde).__name__)} ({e}); pass "
+                            f"{what}_serde=... or in_memory=True") from e
+        if what == "key":
+            try:
+                ok = back == obj and hash(back) == hash(obj)
+            except TypeError:
+                ok = False
+            if not ok:
+                raise TypeError(f"CEPProcessor checkpoint: the key {obj!r} comes back from "
+                                f"{getattr(serde, '__name__', type(serde).__name__)} as {back!r}")
 
     def punctuate(self, timestamp: int) -> None:
         """CEPProcessor.java:167-169 (empty there): forwards what is buffered, then commits

@@ -46,7 +46,7 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False, stream: bo
     # $CEP_LANE_DEFINES="A=1 B=2": tuning knobs of nfa_lane.h for this build (tests of the knobs)
     src = "".join(f"#define {d.replace('=', ' ', 1)}\n" for d in os.environ.get("CEP_LANE_DEFINES", "").split()) + src
     deps = "".join(open(os.path.join(CSRC, h)).read() for h in
-                   ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_coop.h", "nfa_lane.h"))
+                   ("cep_layout.h", "kernel_args.h", "dewey.h", "java.h", "nfa_lane.h"))
     deps += open(os.path.join(HERE, "lane_cpu", "driver.cpp")).read()
     deps += open(os.path.join(HERE, "lane_cpu", "hip", "hip_runtime.h")).read()
     deps += open(os.path.join(HERE, "lane_cpu", "wave_emu.h")).read()

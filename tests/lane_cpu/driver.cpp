@@ -201,66 +201,10 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   if (const char* sp = std::getenv("CEP_LANE_SPREAD")) {
     if (n_q == 1) {
       a.spread = std::strtoull(sp, nullptr, 10);
-      a.spread_snake = 1;
-    }
-  }
-  // $CEP_LANE_SOLO=T (kernel groups, session.cpp solo jobs): the first T keys' jobs run one per
-  // wave, alone (lane 0), before the persistent lanes claim the rest from job T * n_q
-  uint32_t solo_jobs = 0;
-  if (const char* so = std::getenv("CEP_LANE_SOLO")) {
-    if (!streaming && n_q > 1) solo_jobs = (uint32_t)std::min<uint64_t>(std::strtoull(so, nullptr, 10), nk / 4) * n_q;
-  }
-  if (solo_jobs) {
-    NfaArgs b = a;
-    b.solo = 1;
-    b.n_jobs = solo_jobs;
-    b.job_next = nullptr;
-    std::vector<v4u> rs(ring_bytes(8, (uint64_t)solo_jobs * 64, rcap) / 16 + 64);
-    scribble(rs.data(), rs.size() * 16);
-    const uint32_t pl = put_log_entries(rcap);
-    std::vector<v4u> ws(walkq_bytes((uint64_t)solo_jobs * 64, 64, pl) / 16 + 64);
-    scribble(ws.data(), ws.size() * 16);
-    b.rings = rs.data();
-    b.rcap = rcap;
-    b.walks = ws.data();
-    b.wcap = 64;
-    b.plog = pl;
-    b.defer = (uint32_t)defer;
-    blockDim.x = 256;
-    for (uint64_t s2 = 0; s2 < (uint64_t)solo_jobs * 64; s2 += 64) {  // (lanes 1-63 idle)
-      if (std::getenv("CEP_LANE_WAVES")) {
-        emu::run_wave((unsigned)(s2 / 256), (unsigned)(s2 % 256), wave_body, &b);
-      } else {
-        blockIdx.x = (unsigned)(s2 / 256);
-        threadIdx.x = (unsigned)(s2 % 256);
-        cep_nfa_jit(b);
-      }
     }
   }
   // (spread: three idle waves past the W, as the grid's last block can hold)
-  if (solo_jobs) {
-    job_next = solo_jobs;
-    a.job_next = &job_next;
-    a.n_jobs = jobs;
-    const uint32_t pl = put_log_entries(rcap);
-    std::vector<v4u> rs(ring_bytes(8, 64, rcap) / 16 + 64), ws(walkq_bytes(64, 64, pl) / 16 + 64);
-    scribble(rs.data(), rs.size() * 16);
-    a.rings = rs.data();
-    a.rcap = rcap;
-    a.walks = ws.data();
-    a.wcap = 64;
-    a.plog = pl;
-    a.defer = (uint32_t)defer;
-    blockDim.x = 256;
-    if (std::getenv("CEP_LANE_WAVES")) {
-      emu::run_wave(0, 0, wave_body, &a);
-    } else {
-      blockIdx.x = 0;
-      threadIdx.x = 0;
-      cep_nfa_jit(a);
-    }
-    a.job_next = nullptr;
-  } else if (const char* si = std::getenv("CEP_LANE_STREAM_ISO"); si && streaming && n_q == 1 && !a.spread) {
+  if (const char* si = std::getenv("CEP_LANE_STREAM_ISO"); si && streaming && n_q == 1 && !a.spread) {
     // (session.cpp $CEP_STREAM_ISO: the first K keys alone in their waves, the rest 64 per wave)
     const uint64_t k = std::min<uint64_t>(std::strtoull(si, nullptr, 10), nk / 2);
     a.spread_iso = (uint32_t)k;

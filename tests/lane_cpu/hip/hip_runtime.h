@@ -64,10 +64,8 @@ inline unsigned atomicOr(unsigned* p, unsigned v) {
   return o;
 }
 inline void __syncthreads() {}  // (the NFA kernels do not synchronise their waves)
-// a wave of one lane (no emulated wave): the coop pages (nfa_coop.h) need a whole wave
 #define CEP_HOST_LANES 1
-#define CEP_COOP_TESTS 1  // (compile.cpp: the coop pages on every qualifying query and build)
-inline bool cep_host_single_lane() { return emu::g_wave == nullptr; }
+inline bool cep_host_single_lane() { return emu::g_wave == nullptr; }  // (a wave of one lane)
 
 #define CEP_EMU_SITE __FILE__ ":" CEP_EMU_STR(__LINE__)
 #define CEP_EMU_STR(x) CEP_EMU_STR2(x)

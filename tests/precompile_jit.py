@@ -67,7 +67,7 @@ def _compile(ir):
 def main(bench_only=False, workers=None):
     irs = _irs(bench_only)
     t = time.time()
-    os.environ["CEP_JIT_TOUCH"] = "1"  # cache hits refresh their entry's mtime (jit.cpp)
+    # (cep_jit_precompile*: a cache hit refreshes its entry's mtime, jit.cpp)
     with ProcessPoolExecutor(workers or min(8, os.cpu_count() or 1)) as ex:
         spent = list(ex.map(_compile, irs)) + list(ex.map(_compile_group, _group_sets()))
     pruned = 0

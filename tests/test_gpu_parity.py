@@ -278,28 +278,6 @@ def test_cfg5_group_capacity_retry():
         assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
 
 
-def test_solo_and_isolate_knobs(monkeypatch):
-    """The measurement knobs' launch layouts stay exact: a kernel group with its heaviest keys'
-    jobs alone in waves beside the persistent launch ($CEP_SOLO_KEYS, NfaArgs.solo, a second
-    stream), and an underfilled single-query launch with its heaviest ranks alone in their
-    waves ($CEP_ISOLATE, NfaArgs.spread_iso)."""
-    cfg = W.SynthConfig("t", "stock", 300, 500, 0xCE90000 + 5)
-    off, cols = W.generate(cfg)
-    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)[48:]]
-    monkeypatch.setenv("CEP_SOLO_KEYS", "8")  # (knobs are read when a session is made)
-    s = N.Session(qs)
-    s.push(off, cols)
-    for i, q in enumerate(qs):
-        assert_parity(session_result(s, i, off), oracle.run(q.ir, off, cols, threads=8), off)
-    monkeypatch.delenv("CEP_SOLO_KEYS")
-    monkeypatch.setenv("CEP_ISOLATE", "16")
-    cfg = W.SynthConfig("t", "stock", 2000, 400, 0xCE90000 + 3)
-    off, cols = W.generate(cfg)
-    ir = W.stock_query("readme").to_ir()
-    s = N.Session(N.Query(ir))
-    assert_parity(gpu_run(ir, off, cols, session=s), oracle.run(ir, off, cols, threads=8), off)
-
-
 def test_mixed_session_groups():
     """Queries of different shapes in one session: stock variants share a group, the
     any-Kleene query and the zeroOrMore variant run alone, the strict query on the stencil."""

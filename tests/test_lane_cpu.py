@@ -148,21 +148,6 @@ def test_lane_spread(streaming, monkeypatch):
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
 
 
-@pytest.mark.parametrize("waves", [False, True])
-def test_lane_group_solo(waves, monkeypatch):
-    """Kernel groups with solo jobs (session.cpp run_nfa, NfaArgs.solo): the first keys' jobs
-    one per wave alone, the persistent lanes claiming the rest past them - config 5's variants
-    query by query against the oracle."""
-    monkeypatch.setenv("CEP_LANE_SOLO", "5")
-    if waves:
-        monkeypatch.setenv("CEP_LANE_WAVES", "1")
-    cfg = W.SynthConfig("t", "stock", 40, 400, 0xCE90000 + 5)
-    off, cols = W.generate(cfg)
-    irs = [p.to_ir() for p in W.multi_queries(64)[48:64]]
-    for ir, g in zip(irs, lane_cpu.run_group(irs, off, cols)):
-        lane_cpu.assert_same(g, oracle.run(ir, off, cols), off)
-
-
 def test_lane_stream_isolated_keys(monkeypatch):
     """A stream's launch with its first keys alone in their waves and the rest 64 per wave from
     there (session.cpp $CEP_STREAM_ISO, NfaArgs.spread_iso without spread), in emulated waves."""
@@ -357,8 +342,7 @@ def test_lane_whole_waves(case, persist, monkeypatch):
     """The same lane code run as whole 64-lane waves (tests/lane_cpu/wave_emu.h: every lane a
     fiber, each cross-lane operation a rendezvous of the wave's live lanes), so the wave-wide
     drains, partial drains and job claiming see their real neighbours: equal to the oracle.
-    persist False: one lane per key as libcep launches single queries - the wave-cooperative
-    record pages (nfa_coop.h) step the records, as do streams."""
+    persist False: one lane per key as libcep launches single queries and streams."""
     import stream_split as SS
     monkeypatch.setenv("CEP_LANE_WAVES", "1")
     if not persist:
@@ -392,10 +376,10 @@ def test_lane_whole_waves(case, persist, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", [3, 21, 80, 393, 571])
-def test_lane_coop_conflicts_and_partial_drains(seed, monkeypatch):
-    """The wave-cooperative record pages (nfa_coop.h, whole waves) under forced partial drains
-    and a small drain threshold, on fuzz streams whose deferred walks conflict with later puts
-    (the put stamps come from the pages): per batch and as a stream (wide build, put log)."""
+def test_lane_whole_wave_conflicts_and_partial_drains(seed, monkeypatch):
+    """Whole 64-lane waves, one lane per key, under forced partial drains and a small drain
+    threshold, on fuzz streams whose deferred walks conflict with later puts: per batch and as
+    a stream (wide build, put log)."""
     import stream_split as SS
     monkeypatch.setenv("CEP_LANE_WAVES", "1")
     monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
@@ -415,8 +399,9 @@ def test_lane_coop_conflicts_and_partial_drains(seed, monkeypatch):
     assert SS.merge(outs) == SS.oracle_per_key(r, off)
 
 
-def test_lane_coop_small_queue_retry(monkeypatch):
-    """Pages whose records overflow a 2-record run queue: the key is re-run (KE_RETRY), exact."""
+def test_lane_whole_wave_small_queue_retry(monkeypatch):
+    """Whole waves whose records overflow a 2-record run queue: the key is re-run (KE_RETRY),
+    exact."""
     monkeypatch.setenv("CEP_LANE_WAVES", "1")
     monkeypatch.setenv("CEP_LANE_NO_PERSIST", "1")
     cfg = W.SynthConfig("t", "stock", 100, 400, 0xCE90000 + 3)

@@ -110,3 +110,46 @@ def test_launch_path_reads_no_environment():
             assert "getenv" not in src, f
     ses = open(os.path.join(csrc, "session.cpp")).read()
     assert "tuning_from_env()" in ses and ses.count("tuning_from_env") == 1
+
+
+def _release_getenv_calls(src: str) -> list:
+    """getenv("...") names outside `#ifdef CEP_MEASURE` regions (nested #if blocks tracked)"""
+    names, stack = [], []
+    for line in src.splitlines():
+        t = line.strip()
+        if t.startswith("#if"):
+            stack.append(t == "#ifdef CEP_MEASURE")
+        elif t.startswith("#else") and stack:
+            stack[-1] = False if stack[-1] else stack[-1]
+        elif t.startswith("#endif") and stack:
+            stack.pop()
+        elif not any(stack):
+            code = re.sub(r"//.*", "", line)
+            names += re.findall(r'getenv\(\s*("?[A-Za-z_]*"?)', code)
+    return names
+
+
+def test_release_build_reads_only_jit_cache():
+    """ The release libcep.so reads one environment variable,
+    $CEP_JIT_CACHE: every tuning knob is compiled in only under CEP_MEASURE (the measurement
+    build, libcep_measure.so); and a knob set in the environment changes nothing the release
+    build generates."""
+    csrc = os.path.join(ROOT, "kafkastreams-cep_amd", "csrc")
+    found = []
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".cpp", ".hip", ".h")):
+            found += [(f, n) for n in _release_getenv_calls(open(os.path.join(csrc, f)).read())]
+    assert found == [("jit.cpp", '"CEP_JIT_CACHE"')], found
+    ir = W.stock_query("readme").to_ir()
+    base = N.Query(ir).jit_source
+    env = {"CEP_WALK_FLUSH": "7", "CEP_PROF": "1", "CEP_DEWEY_PAIRS": "5", "CEP_JIT_WAVES": "4", "CEP_RING_LDS": "1"}
+    saved = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update(env)
+        assert N.Query(ir).jit_source == base
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v

@@ -384,9 +384,94 @@ def test_checkpoint_is_plain_data():
         def __init__(self, name, price, volume):
             self.name, self.price, self.volume = name, price, volume
 
+    #  an attribute-style value the default serde cannot encode fails at its first
+    # record, not at the next commit; in memory it needs no serde at all
     proc3 = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
     ctx3 = P.RecordContext("StockEvents", 0, stores={})
     proc3.init(ctx3)
-    ctx3.send("k", Obj("e1", 100, 1010), 0)
     with pytest.raises(TypeError):
-        proc3.punctuate(0)
+        ctx3.send("k", Obj("e1", 100, 1010), 0)
+    proc4 = P.CEPProcessor(W.stock_query("readme"), in_memory=True, batch_size=3, session_factory=OracleStreamSession)
+    ctx4 = P.RecordContext("StockEvents", 0)
+    proc4.init(ctx4)
+    for k, v, ts in _readme_records():
+        ctx4.send(k, Obj(**v), ts)
+    proc4.close()
+    ref_ctx, _ = run_records(W.stock_query("readme"), _readme_records(), 3, gpu=False)
+    assert forwarded_view(ctx4) == forwarded_view(ref_ctx) and len(ctx4.forwarded) == 4
+
+
+class _Obj:
+    def __init__(self, name, price, volume):
+        self.name, self.price, self.volume = name, price, volume
+
+    def __eq__(self, o):
+        return isinstance(o, _Obj) and vars(self) == vars(o)
+
+
+class _ObjSerde:
+    """a user value serde for attribute-style values"""
+
+    @staticmethod
+    def serialize(o):
+        return json.dumps([o.name, o.price, o.volume]).encode()
+
+    @staticmethod
+    def deserialize(b):
+        return _Obj(*json.loads(b.decode()))
+
+
+def test_json_serde_keeps_types():
+    """ the default checkpoint serde gives back what it was given: tuple keys, dicts
+    with non-string keys, bytes, non-finite floats, numpy scalars."""
+    for x in [("AAPL", 3), {"a": (1, 2), 5: [None, True]}, {"__cep__": 1}, b"\x00\xff", float("inf"),
+              np.int32(7), np.float64(2.5), [("x",), {}], "s", 12, None]:
+        y = P.JsonSerde.deserialize(P.JsonSerde.serialize(x))
+        assert y == x and type(y) is type(x), (x, y)
+    assert np.isnan(P.JsonSerde.deserialize(P.JsonSerde.serialize(float("nan"))))
+    with pytest.raises(TypeError):
+        P.JsonSerde.serialize({1, 2})
+
+
+@pytest.mark.parametrize("user_serde", [False, True])
+def test_restart_tuple_keys_and_object_values(user_serde):
+    """ a persistent processor over tuple keys - and, with a user value serde,
+    attribute-style values - restores from its checkpoint and forwards what an uninterrupted
+    one forwards (the same Sequences, the same key and value objects)."""
+    recs = random_records(13, n_keys=8, n=240)
+    recs = [((k, int(k[1:])), (_Obj(**v) if user_serde else dict(v, extra={1: (2, 3)})), ts) for k, v, ts in recs]
+    q = W.stock_query("readme")
+    kw = dict(batch_size=16, max_keys=64, session_factory=OracleStreamSession,
+              value_serde=_ObjSerde if user_serde else None)
+    ref_ctx = P.RecordContext("StockEvents", 1)
+    ref = P.CEPProcessor(q, **kw)
+    ref.init(ref_ctx)
+    for i, (k, v, ts) in enumerate(recs):
+        ref_ctx.send(k, v, ts, offset=i)
+    ref.close()
+    stores = {}
+    ctx = P.RecordContext("StockEvents", 1, stores=stores)
+    proc = P.CEPProcessor(q, **kw)
+    proc.init(ctx)
+    n_at_commit = 0
+    for i, (k, v, ts) in enumerate(recs[:150]):
+        ctx.send(k, v, ts, offset=i)
+        if i == 119:
+            proc.punctuate(ts)
+            n_at_commit = len(ctx.forwarded)
+    # crash after record 149; the restored processor gets records 120.. again
+    ctx2 = P.RecordContext("StockEvents", 1, stores=stores)
+    proc2 = P.CEPProcessor(q, **kw)
+    proc2.init(ctx2)
+    assert all(isinstance(k, tuple) for k in proc2._keys)
+    for i, (k, v, ts) in enumerate(recs[120:], start=120):
+        ctx2.send(k, v, ts, offset=i)
+    proc2.close()
+
+    def view(c):
+        return [[(st, [(e.key, e.offset, e.value) for e in evs]) for st, evs in sq.as_map().items()]
+                for _, sq in c.forwarded]
+
+    want = view(ref_ctx)
+    assert len(want) > 5
+    assert view(ctx)[:n_at_commit] + view(ctx2) == want
