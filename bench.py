@@ -280,6 +280,8 @@ def cfg4(device, stream, steps, warmup, dist, threads, cpu_every, stress=True):
     alg = 8.0 * stream.n_events + 4.0 * n_pairs + 4.0 * n_m
     what = ("S1 also folds volume, S2 reads it with getOrElse: no key throws" if stress else
             "the query as written (parity case; NPE in the reference on the keys counted in key_errors)")
+    # priced at step level, like cfg4_semantic: the step streams the
+    # columns once (begin-hit bitmap), while cep_nfa_jit skips quiet words and keys that threw
     res = {"workload": f"cfg4: skip_till_any Kleene+ with folds avg/sum, within 10 ms, {what}; {stream.n_keys} keys x "
                        f"~1000 events ({stream.n_events} events) on 1 GPU",
            "value": stream.n_events * steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / steps,
@@ -288,8 +290,9 @@ def cfg4(device, stream, steps, warmup, dist, threads, cpu_every, stress=True):
            "buffer_nodes_per_key": st["nodes_used"] / max(1, stream.n_keys),
            "buffer_preds_per_key": st["preds_used"] / max(1, stream.n_keys),
            "retried_jobs": st["retried_jobs"],
-           "roofline": roofline(alg, st["main_ms"], "cep_nfa_jit", "cep_nfa_jit_cfg4" + ("s" if stress else ""),
-                                step_kernels_ms=kms)}
+           "roofline": roofline(alg, 1e3 * el / steps, "whole step (cep_nfa_bits, cep_nfa_est, lane order, "
+                                "cep_nfa_jit, compaction)", "cfg4" + ("s" if stress else "") + "_step",
+                                cep_nfa_jit_ms=st["main_ms"], step_kernels_ms=kms)}
     if cpu_every:
         cfg = W.SynthConfig("cfg4", "stock", stream.n_keys, 1000, W.CONFIGS[3].seed)
         res["cpu_baseline"] = cpu_baseline(cfg, [p], threads, cpu_every, gpu_digests([p], device), extrapolated=True)
@@ -504,29 +507,41 @@ def cfg5(device, n_keys, sub, steps, warmup, threads, cpu_every):
 def end_to_end(args, device, dist):
     """SURVEY §8(d)'s secondary figure: the same cfg-3 workload handed over in arrival order
     (a key id per event, round-robin interleaved), so each step includes the device partition
-    (csrc/partition.hip) before the NFA."""
+    (csrc/partition.hip) before the NFA.  Per step the record keeps what the push spent (VERDICT
+    r4 item 5: one round-4 run measured its NFA launches at 185 ms against the usual 31): the
+    partition, the matching launch alone, bitmap + estimate + lane order, re-runs, and the device
+    allocations the push made."""
     cfg = W.CONFIGS[3]
     st = N.synth_arrival_stream("stock", cfg.seed, args.keys, args.mean, 0, device)
     q = N.Query(W.stock_query(args.variant).to_ir())
     s = N.Session(q, device=device)
     for _ in range(max(1, args.warmup)):
         s.push_arrival_device(st)
-    part, kern = [], []
+    steps = []
     dist.barrier()
     N.lib().cep_sync(s.h)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         s.push_arrival_device(st)
-        part.append(_partition_ms(s))
-        kern.append(s.timing(0)[0])
+        b = s.stats(0)
+        steps.append({"partition_ms": _partition_ms(s), "nfa_kernel_ms": b["kernel_ms"], "main_ms": b["main_ms"],
+                      "est_order_bits_ms": b["kernel_ms"] - b["main_ms"] - b["retry_ms"], "retry_ms": b["retry_ms"],
+                      "retried_jobs": int(b["retried_jobs"]), "allocs": int(b["allocs"])})
     N.lib().cep_sync(s.h)
     el = time.perf_counter() - t0
     n_m, _ = s.digest(0)
+    try:
+        bal, _ = s.lane_balance(0)
+    except N.CepError:
+        bal = None
     s.close()
+    mean = lambda k: float(np.mean([x[k] for x in steps]))  # noqa: E731
     return {"workload": "cfg3 stock query, arrival-order batches (partition on the GPU + NFA)",
             "value": st.n_events * args.steps / el, "unit": "events/s", "ms_per_step": 1e3 * el / args.steps,
-            "partition_ms": float(np.mean(part)), "nfa_kernel_ms": float(np.mean(kern)),
-            "matches_per_step": n_m}
+            "partition_ms": mean("partition_ms"), "nfa_kernel_ms": mean("nfa_kernel_ms"), "main_ms": mean("main_ms"),
+            "est_order_bits_ms": mean("est_order_bits_ms"), "retry_ms": mean("retry_ms"),
+            "retried_jobs": sum(x["retried_jobs"] for x in steps), "allocs": sum(x["allocs"] for x in steps),
+            "lane_balance": bal, "per_step": steps, "matches_per_step": n_m}
 
 
 def ingest(device, steps, keys, cpu_sample):

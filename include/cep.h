@@ -279,7 +279,8 @@ typedef struct {
                               the stream build's 3 pairs, continued by the wide build) */
   uint64_t nodes_used, preds_used, out_chunks_used;  /* buffer pools at the end of the batch */
   uint32_t launches;
-  uint32_t heavy_first;    /* reserved (0): the heavy-first job order was measured slower and removed */
+  uint32_t allocs;         /* device allocations the last cep_push_batch made (0 once a session has
+                              seen a batch of this shape: buffers and pools are reused) */
 } cep_batch_stats;
 int cep_last_stats(cep_session* s, int query, cep_batch_stats* out);
 

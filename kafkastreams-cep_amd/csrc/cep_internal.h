@@ -134,6 +134,7 @@ hipError_t partition(const uint32_t* key, uint64_t n, uint64_t n_keys, int nf, C
 // est_sorted: the sorted keys (inverted), key16: n words (tmp: scratch grown as needed)
 hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,
                              uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st);
+hipError_t sort_keys_scratch(uint64_t n, void*& tmp, size_t& tmp_bytes);
 std::string jit_cache_key(const std::string& src);
 hipError_t gather_keys(uint64_t n_sel, const uint32_t* sel, const uint64_t* src_off, const uint64_t* dst_off,
                        int nf, const uint32_t* col_bytes, const void* const* src_cols, void* const* dst_cols,

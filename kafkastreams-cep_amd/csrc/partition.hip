@@ -360,8 +360,9 @@ __global__ void __launch_bounds__(256) est_key16(const uint32_t* __restrict__ es
   }
 }
 
-hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,
-                             uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
+// the scratch sort_keys_by_work needs for n keys, (re)allocated if `tmp` is smaller (the
+// caller does this before its timed interval)
+hipError_t sort_keys_scratch(uint64_t n, void*& tmp, size_t& tmp_bytes) {
   const size_t need = lsd_scratch_bytes(n, 16);
   if (need > tmp_bytes) {
     if (tmp) (void)hipFree(tmp);
@@ -371,6 +372,13 @@ hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t
     if (e != hipSuccess) return e;
     tmp_bytes = need;
   }
+  return hipSuccess;
+}
+
+hipError_t sort_keys_by_work(const uint32_t* est, uint32_t* est_sorted, uint32_t* key16, uint32_t* order,
+                             uint64_t n, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
+  const hipError_t e = sort_keys_scratch(n, tmp, tmp_bytes);
+  if (e != hipSuccess) return e;
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(est_key16, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, est, key16, n);
   return lsd_sort(key16, n, 16, true, 0, est_sorted, order, tmp, tmp_bytes, nullptr, st);

@@ -47,6 +47,8 @@ struct HipError : std::runtime_error {
 // on stderr, ms.  Set when a session is created with the knob.
 static bool g_host_trace = false;
 static bool host_trace() { return g_host_trace; }
+// device allocations made (DBuf ensure / grow_keep): cep_batch_stats.allocs counts a batch's
+static thread_local uint32_t g_allocs = 0;
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -67,6 +69,7 @@ struct DBuf {
     if (p) HIPCHECK(hipFree(p));
     p = nullptr;
     bytes = 0;
+    g_allocs++;
     n = std::max<size_t>(n, 256);
     if (hipMalloc(&p, n) != hipSuccess) {
       p = nullptr;
@@ -86,6 +89,7 @@ struct DBuf {
       }
     } tr{t0, n};
     void* q = nullptr;
+    g_allocs++;
     if (hipMalloc(&q, n) != hipSuccess) throw std::bad_alloc();
     if (p && keep) HIPCHECK(hipMemcpyAsync(q, p, std::min(keep, bytes), hipMemcpyDeviceToDevice, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -242,6 +246,7 @@ struct cep_session {
   DBuf heavy;  // heavy-key list of the output scatter
   DBuf rings, walks, nodes, preds, preds0, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
   DBuf prof;  // measurement runs ($CEP_PROF): the main launch's time split (nfa_lane.h)
+  uint32_t last_allocs = 0;  // device allocations the last cep_push_batch made
 };
 
 namespace {
@@ -305,7 +310,8 @@ void run_stencil(cep_session* s, QueryRt& r) {
   s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
   s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));                     // a match word per 64 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
-  s->bnd.ensure(sizeof(uint32_t) * 2 * (s->n_events / 64 + 2));                   // word -> key, sequence number
+  const uint64_t nw4 = (s->n_events / 64 + 2 + 3) & ~3ull;  // (word_seq 16-B aligned: stencil_emit's loads)
+  s->bnd.ensure(sizeof(uint32_t) * 2 * nw4);                                     // word -> key, sequence number
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
   if (!r.h_sc) {
@@ -336,7 +342,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   a.key_off = s->key_off;
   a.wave_key = s->keylist.as<uint32_t>();
   a.word_key = s->bnd.as<uint32_t>();
-  a.word_seq = a.word_key + (s->n_events / 64 + 2);
+  a.word_seq = a.word_key + nw4;
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.cols = s->cols;
@@ -592,14 +598,27 @@ void run_nfa(cep_session* s, GroupRt& g) {
 
   float total_ms = 0;
   uint32_t launches = 0;
-  HIPCHECK(hipEventRecord(s->ev0, s->stream));
   const bool wm_here = s->wm_fold && &g == s->groups[0].get();
-  if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
+  // (every buffer of the timed interval below is allocated before its first event: an
+  // allocation there would count its host time - hipFree synchronises - as kernel time)
+  const uint64_t nb_bits = (s->n_events + 256 * kBitStrips - 1) / (256 * kBitStrips);
+  if (g.fn_bits && s->n_events) {
     s->bhits.ensure(8 * ((s->n_events + 63) / 64));
+    if (wm_here) s->wm_blocks.ensure(8 * nb_bits);
+  }
+  if (g.fn_est && nk > 64) {
+    g.est.ensure(4 * nk);
+    g.est_sorted.ensure(4 * nk);
+    g.order.ensure(4 * nk);
+    g.order_tmp.ensure(4 * nk);
+    HIPCHECK(sort_keys_scratch(nk, g.sort_tmp, g.sort_tmp_bytes));
+  }
+  if (s->tune.prof) s->prof.ensure(16 * sizeof(unsigned long long));
+  HIPCHECK(hipEventRecord(s->ev0, s->stream));
+  if (g.fn_bits && s->n_events) {  // begin-hit bitmap: quiet lanes skip 64 events per load
     a.bhits = s->bhits.as<uint64_t>();
-    const uint64_t nb = (s->n_events + 256 * kBitStrips - 1) / (256 * kBitStrips);
+    const uint64_t nb = nb_bits;
     if (wm_here) {  // (run_nfa's scratch memset above cleared wmax)
-      s->wm_blocks.ensure(8 * nb);
       a.wm_blocks = s->wm_blocks.as<int64_t>();
       a.n_wm_blocks = nb;
       a.wmax = &sc->wmax;
@@ -611,10 +630,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // start first.  (A stream's run queues live at the key's position, so its lanes too may run
   // in any order; its estimate adds the runs each key carries.)
   if (g.fn_est && nk > 64) {
-    g.est.ensure(4 * nk);
-    g.est_sorted.ensure(4 * nk);
-    g.order.ensure(4 * nk);
-    g.order_tmp.ensure(4 * nk);
     a.est = g.est.as<uint32_t>();
     a.est_blend = streaming && !s->tune.no_est_blend ? 1u : 0u;  // ($CEP_NO_EST_BLEND: measurement runs)
     const uint64_t eg = est_lanes(s->n_events, nk);  // lanes per key
@@ -629,7 +644,6 @@ void run_nfa(cep_session* s, GroupRt& g) {
   }
   const bool prof = s->tune.prof;  // (the query must be compiled with it too)
   if (prof) {
-    s->prof.ensure(16 * sizeof(unsigned long long));
     HIPCHECK(hipMemsetAsync(s->prof.p, 0, 16 * sizeof(unsigned long long), s->stream));
     a.prof = s->prof.as<unsigned long long>();
   }
@@ -1177,7 +1191,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     return fail(CEP_E_INVALID, "a batch holds < 2^32 keys and events (sequence numbers are u32)");
   if (b->arrival_key && b->n_events >= 0x80000000ull)
     return fail(CEP_E_INVALID, "an arrival-order batch holds < 2^31 events (split it)");
-  return guarded([&] {
+  const uint32_t allocs0 = g_allocs;
+  const int rc = guarded([&] {
     DeviceGuard g(s->device);
     const cep_query* q0 = s->qs[0]->q;
     const uint32_t nf = q0->info.n_fields;
@@ -1250,6 +1265,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b) {
     if (host_trace()) std::fprintf(stderr, "cep_host run_nfa %.2f ms\n", now_ms() - t0);
     for (auto& r : s->qs) r->have = true;
   });
+  s->last_allocs = g_allocs - allocs0;
+  return rc;
 }
 
 int cep_batch_layout(cep_session* s, int memory, const uint64_t** key_off, const uint32_t** arrival_index,
@@ -1604,10 +1621,12 @@ int cep_last_stats(cep_session* s, int query, cep_batch_stats* out) {
       out->group = 0xFFFFFFFFu;
       out->kernel_ms = out->main_ms = r.kernel_ms;
       out->launches = r.launches;
+      out->allocs = s->last_allocs;
       return;
     }
     *out = s->groups[r.group]->stats;
     out->group = (uint32_t)r.group;
+    out->allocs = s->last_allocs;
   });
 }
 

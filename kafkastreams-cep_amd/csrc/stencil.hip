@@ -188,11 +188,14 @@ struct WaveMask {
 // windows crossing a key start are settled after the loop, on the natural words, with vector
 // work.  (This keeps the loop's scalar registers down - 58 instead of 106, 8 waves per SIMD
 // instead of 6 - and the pass at ~75 us for 1e8 events instead of ~90: profiles/r05/.)
-template <int M, bool RANGE, int NCOL>
+// FULL: the launch holds whole waves of the range fast path only (aligned columns, no empty
+// range: run_stencil's full tiles) - the slow path's code and its registers are compiled out
+template <int M, bool RANGE, int NCOL, bool FULL>
 __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t wbase, const int lane, WaveMask& out) {
+  static_assert(!FULL || RANGE, "the full-wave build is the range fast path");
   constexpr int H = M - 1;              // events a window reaches back
   const StEval<M, RANGE, NCOL> ev(A);
-  const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never;
+  const bool fast = FULL || (RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never);
   // The fast path's first step is requested before anything else: the key-start words and
   // the seed events below are dependent round trips
   const v4i* c0 = reinterpret_cast<const v4i*>(A.col[0] + wbase) + lane;
@@ -336,7 +339,7 @@ __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t w
       ya = NCOL > 1 ? __builtin_nontemporal_load(c1 + qn * 64) : xa;
       step(q + 1, xb, yb, std::true_type{});
     }
-  } else {
+  } else if constexpr (!FULL) {
     const v4i z = {0, 0, 0, 0};
     for (int q = 0; q < kStSteps; q++) step(q, z, z, std::false_type{});
   }
@@ -359,7 +362,7 @@ __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t w
 #pragma unroll
     for (int s = 0; s < M; s++) P[s] = 0;
     if (sv) {
-      if (RANGE) ev.range(sx0, sx1, P, 0);
+      if constexpr (RANGE) ev.range(sx0, sx1, P, 0);
       else ev.one(A, (uint64_t)sp, P, 0);
     }
     uint64_t seed = wbase >= (uint64_t)H ? (1ull << H) - 1ull : 0ull;
@@ -386,15 +389,19 @@ __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t w
 
 // Pass 1: per wave the mask phase, its natural words, their keys and sequence numbers, and
 // the match count per tile (and per 64 tiles, for stencil_emit's offsets)
-template <int M, bool RANGE, int NCOL>
-__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
+// (the full-wave build at 8 waves per SIMD: the scalar registers of the step loop bound its
+// occupancy - 99 SGPRs: 6 waves - and the pass streams better with more waves in flight)
+template <int M, bool RANGE, int NCOL, bool FULL>
+__global__ void __launch_bounds__(kStThreads) __attribute__((amdgpu_waves_per_eu(FULL ? 8 : 1)))
+stencil_mask(StencilArgs A) {
   __shared__ uint32_t s_cnt[kStThreads / 64];
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
   // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t wbase = (uint64_t)blockIdx.x * kStTile + (uint64_t)wv * kStWave;
+  const uint64_t tile = A.tile0 + blockIdx.x;
+  const uint64_t wbase = tile * kStTile + (uint64_t)wv * kStWave;
   WaveMask o;
-  wave_mask<M, RANGE, NCOL>(A, wbase, lane, o);
+  wave_mask<M, RANGE, NCOL, FULL>(A, wbase, lane, o);
   const uint64_t ws = wbase + (uint64_t)lane * 64;
   // (bit 31: a key starts inside the word after its first event - stencil_emit walks key_off
   // there; elsewhere a match's sequence number is word_seq + its offset in the word)
@@ -411,52 +418,68 @@ __global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-    A.tile_cnt[blockIdx.x] = c;
-    if (c) atomicAdd(A.group_cnt + blockIdx.x / kStGroup, c);  // per 64 tiles, for stencil_emit
+    A.tile_cnt[tile] = c;
+    if (c) atomicAdd(A.group_cnt + tile / kStGroup, c);  // per 64 tiles, for stencil_emit
   }
 }
 
-// Pass 2: a thread per 64-event word, the tile's offset from the group and tile counts, a
-// block scan for the threads' offsets.  A match's key is the thread's first key (word_key)
-// advanced over the key offsets it passes.
+// Pass 2: a thread per kEmW consecutive 64-event words (a block: kEmW mask tiles), the block's
+// offset from the group and tile counts, a block scan for the threads' offsets.  A match's key
+// is its word's first key (word_key) advanced over the key offsets it passes.  (One word per
+// thread ran 6104 blocks for 1e8 events, three rounds of resident blocks each paying a load
+// and a store round trip: ~18 us; kEmW words per thread issue their loads together and the
+// grid fits the chip in one round.)
+constexpr int kEmW = 4;
+constexpr uint32_t kEmStage = 3072;  // matches staged in LDS (24 KB: 6 blocks per CU)
+
 template <int M>
 __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
-  // a tile's matches are staged in LDS and written out contiguously (coalesced) when they fit
-  constexpr uint32_t kStage = 2048;
   __shared__ uint32_t s_wsum[kStThreads / 64];
   __shared__ uint64_t s_toff[kStThreads / 64];
-  __shared__ uint2 s_stage[kStage];  // (key, sequence number of the final event)
+  __shared__ uint2 s_stage[kEmStage];  // (key, sequence number of the final event)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint64_t t = blockIdx.x;
-  const uint64_t p0 = t * kStTile + (uint64_t)tid * kStPer;
-  // Every independent load is issued before the first use (addresses clamped, no branches):
-  // this thread's word, its first key, and the counts of the tiles before it.
-  const bool valid = p0 < A.n_events;
-  const uint64_t pc = valid ? p0 : t * kStTile;  // a tile's first event always exists
-  const uint64_t w0 = A.mask[pc / 64];
-  const uint32_t wk = A.word_key[pc / 64], seq0 = A.word_seq[pc / 64];
-  uint32_t key = wk & 0x7FFFFFFFu;
-  const bool cross = (wk >> 31) != 0;  // a key starts inside this thread's 64 events
-  uint64_t match = valid ? w0 : 0ull;
-  const uint32_t cnt = (uint32_t)__popcll(match);
-  uint64_t kstart = 0, knext = 0;
-  if (cnt && cross) {
-    kstart = A.key_off[key];
-    knext = A.key_off[key + 1];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kEmW;  // the block's first mask tile
+  const uint64_t n_words = (A.n_events + 63) / 64;
+  const uint64_t w0 = t0 * (kStTile / 64) + (uint64_t)tid * kEmW;  // this thread's first word
+  // Every independent load is issued before the first use: the thread's words (16-B loads:
+  // kEmW is 4, the word index a multiple of 4), their first keys and sequence numbers, and the
+  // counts of the tiles before the block (its offset).
+  uint64_t wm[kEmW];
+  uint32_t wk[kEmW], ws[kEmW];
+  if (w0 + kEmW <= n_words) {
+    const uint4 m01 = *reinterpret_cast<const uint4*>(A.mask + w0);
+    const uint4 m23 = *reinterpret_cast<const uint4*>(A.mask + w0 + 2);
+    const uint4 k4 = *reinterpret_cast<const uint4*>(A.word_key + w0);
+    const uint4 s4 = *reinterpret_cast<const uint4*>(A.word_seq + w0);
+    wm[0] = ((uint64_t)m01.y << 32) | m01.x;
+    wm[1] = ((uint64_t)m01.w << 32) | m01.z;
+    wm[2] = ((uint64_t)m23.y << 32) | m23.x;
+    wm[3] = ((uint64_t)m23.w << 32) | m23.z;
+    wk[0] = k4.x, wk[1] = k4.y, wk[2] = k4.z, wk[3] = k4.w;
+    ws[0] = s4.x, ws[1] = s4.y, ws[2] = s4.z, ws[3] = s4.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < kEmW; i++) {
+      const bool v = w0 + i < n_words;
+      wm[i] = v ? A.mask[w0 + i] : 0ull;
+      wk[i] = v ? A.word_key[w0 + i] : 0u;
+      ws[i] = v ? A.word_seq[w0 + i] : 0u;
+    }
   }
-  // block exclusive scan of the match counts
+  uint64_t part = 0;
+  const uint64_t g0 = (t0 / kStGroup) * kStGroup;
+  for (uint64_t i = tid; i < t0 / kStGroup; i += kStThreads) part += A.group_cnt[i];
+  if (g0 + tid < t0) part += A.tile_cnt[g0 + tid];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < kEmW; i++) cnt += (uint32_t)__popcll(wm[i]);
+  // block exclusive scan of the threads' match counts
   uint32_t incl = cnt;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(incl, o, 64);
     if (lane >= o) incl += y;
   }
-  // this tile's output offset: the groups of 64 tiles before its own, then the tiles of its
-  // group before it (cheaper than a scan launch between the passes)
-  uint64_t part = 0;
-  const uint64_t g0 = (t / kStGroup) * kStGroup;
-  for (uint64_t i = tid; i < t / kStGroup; i += kStThreads) part += A.group_cnt[i];
-  if (g0 + tid < t) part += A.tile_cnt[g0 + tid];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
   if (lane == 63) s_wsum[wv] = incl;
@@ -468,42 +491,55 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
     if (w < wv) woff += s_wsum[w];
   const uint32_t excl = woff + incl - cnt;
   const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
-  if (t + 1 == gridDim.x && tid == kStThreads - 1) {  // all matches
+  if (blockIdx.x + 1 == gridDim.x && tid == kStThreads - 1) {  // all matches
     *A.total = toff + woff + incl;
     if (A.total_host) *A.total_host = toff + woff + incl;  // pinned host memory, read after the batch's event
   }
-  const uint32_t tile_total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  const bool staged = tile_total <= kStage;  // block-uniform
+  const uint32_t block_total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  const bool staged = block_total <= kEmStage;  // block-uniform
   uint64_t o = toff + excl;
-  uint32_t so = excl;  // slot within the tile
-  while (match) {
-    const int i = __builtin_ctzll(match);
-    match &= match - 1;
-    const uint64_t p = p0 + i;
-    uint32_t seq = seq0 + (uint32_t)i;
-    if (cross) {
-      while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
-        key++;
-        kstart = knext;
-        knext = A.key_off[key + 1];
-      }
-      seq = (uint32_t)(p - kstart);
-    }
-    if (staged) {
-      s_stage[so++] = uint2{key, seq};
-    } else if (o < A.out_cap) {
-      A.m_key[o] = key;
+  uint32_t so = excl;  // slot within the block
 #pragma unroll
-      for (int x = 0; x < M; x++) A.p_seq[o * M + x] = seq - x;
-    } else {
-      atomicOr(A.overflow, 1u);
+  for (int i = 0; i < kEmW; i++) {
+    uint64_t match = wm[i];
+    if (!match) continue;
+    const uint64_t p0 = (w0 + i) * 64;
+    uint32_t key = wk[i] & 0x7FFFFFFFu;
+    const bool cross = (wk[i] >> 31) != 0;  // a key starts inside this word
+    uint64_t kstart = 0, knext = 0;
+    if (cross) {
+      kstart = A.key_off[key];
+      knext = A.key_off[key + 1];
     }
-    o++;
+    while (match) {
+      const int b = __builtin_ctzll(match);
+      match &= match - 1;
+      const uint64_t p = p0 + b;
+      uint32_t seq = ws[i] + (uint32_t)b;
+      if (cross) {
+        while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
+          key++;
+          kstart = knext;
+          knext = A.key_off[key + 1];
+        }
+        seq = (uint32_t)(p - kstart);
+      }
+      if (staged) {
+        s_stage[so++] = uint2{key, seq};
+      } else if (o < A.out_cap) {
+        A.m_key[o] = key;
+#pragma unroll
+        for (int x = 0; x < M; x++) A.p_seq[o * M + x] = seq - x;
+      } else {
+        atomicOr(A.overflow, 1u);
+      }
+      o++;
+    }
   }
   if (!staged) return;
   __syncthreads();
   // thread i writes matches i, i + 256, ...: adjacent threads, adjacent slots
-  for (uint32_t i = tid; i < tile_total; i += kStThreads) {
+  for (uint32_t i = tid; i < block_total; i += kStThreads) {
     const uint64_t slot = toff + i;
     const uint2 e = s_stage[i];
     if (slot < A.out_cap) {
@@ -532,10 +568,32 @@ hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n
 
 uint64_t stencil_waves(uint64_t n_events) { return (n_events + kStWave - 1) / kStWave; }
 
+// an empty stage range: no event can be in that stage (StEval::never, the slow path's case)
+static bool range_never(const StencilArgs& a, int m, int ncol) {
+  for (int s = 0; s < m; s++)
+    for (int c = 0; c < ncol; c++)
+      if (a.rs[s].lo[c] > a.rs[s].hi[c] || a.rs[s].lo[c] > INT32_MAX || a.rs[s].hi[c] < INT32_MIN) return true;
+  return false;
+}
+
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
-  hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
-  hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)n_tiles), dim3(kStThreads), 0, st, a);
+  // the tiles whose four waves are all whole fast-path waves run the full-wave build, the
+  // rest (the stream's last tile; every tile of an unaligned or interpreted query) the general one
+  const uint64_t full = RANGE && a.aligned && !range_never(a, M, NCOL) ? a.n_events / kStTile : 0;
+  StencilArgs b = a;
+  if constexpr (RANGE) {
+    if (full) {
+      b.tile0 = 0;
+      hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, true>), dim3((uint32_t)full), dim3(kStThreads), 0, st, b);
+    }
+  }
+  if (full < n_tiles) {
+    b.tile0 = full;
+    hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, false>), dim3((uint32_t)(n_tiles - full)), dim3(kStThreads), 0,
+                       st, b);
+  }
+  hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }
 

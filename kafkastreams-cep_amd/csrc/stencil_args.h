@@ -23,6 +23,7 @@ struct StencilArgs {
   uint16_t prog[kMaxStencil];
   uint16_t stage_name[kMaxStencil];    // walk order: stage name of pair t (t = 0 is the final event)
   bool aligned;              // col[] 16-B aligned: vector loads
+  uint64_t tile0;            // stencil_mask: the launch's first tile (the full-wave and general builds)
   // pass 1 -> pass 3
   uint64_t* mask;            // per 64 events a word: bit i = a match ends at event 64 w + i
   uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1); bit 31: a key

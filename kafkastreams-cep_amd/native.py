@@ -52,7 +52,7 @@ class BatchStats(C.Structure):
     _fields_ = [("group", C.c_uint32), ("group_queries", C.c_uint32), ("kernel_ms", C.c_double),
                 ("main_ms", C.c_double), ("retry_ms", C.c_double), ("retried_jobs", C.c_uint64),
                 ("nodes_used", C.c_uint64), ("preds_used", C.c_uint64), ("out_chunks_used", C.c_uint64),
-                ("launches", C.c_uint32), ("heavy_first", C.c_uint32)]
+                ("launches", C.c_uint32), ("allocs", C.c_uint32)]
 
 
 class Batch(C.Structure):

@@ -155,7 +155,7 @@ int main(int argc, char** argv) {
   hipMalloc(&wk, (n_waves + 1) * 4);
   hipMalloc(&zero, 4096 * 4);
   hipMalloc(&mask, 4 * (n / 256 + 2) * 8);
-  hipMalloc(&word_key, 2 * (n / 64 + 2) * 4);
+  hipMalloc(&word_key, 2 * ((n / 64 + 2 + 3) & ~3ull) * 4);
   hipMalloc(&tile_cnt, (n_tiles + 1) * 4);
   hipLaunchKernelGGL(gen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, v, n);
   hipLaunchKernelGGL(gen_off, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, 0, off, n_keys, n);
@@ -175,13 +175,14 @@ int main(int argc, char** argv) {
   }
   a.mask = mask;
   a.word_key = word_key;
-  a.word_seq = word_key + (n / 64 + 2);
+  a.word_seq = word_key + ((n / 64 + 2 + 3) & ~3ull);
   a.tile_cnt = tile_cnt;
   a.group_cnt = zero;
   const double gb = n * 4.0 / 1e9;
   auto rep = [&](const char* name, float us) { printf("%-28s %8.1f us  %5.2f TB/s\n", name, us, gb / (us * 1e-6) / 1e3); };
   rep("rd (16 KB per wave)", timeit([&] { hipLaunchKernelGGL(rd, dim3((uint32_t)n_tiles), dim3(256), 0, 0, (const v4i*)v, n / 4, out); }));
-  rep("stencil_mask", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1>), dim3((uint32_t)n_tiles), dim3(256), 0, 0, a); }));
+  rep("stencil_mask (general build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3((uint32_t)n_tiles), dim3(256), 0, 0, a); }));
+  rep("stencil_mask (full-wave build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3((uint32_t)(n / kStTile)), dim3(256), 0, 0, a); }));
   a.m_key = (uint32_t*)out;  // (probe: the emit pass's outputs, sized for the synthetic stream's matches)
   uint32_t* pseq;
   uint64_t* tot;
@@ -194,7 +195,21 @@ int main(int argc, char** argv) {
   a.total = tot;
   a.out_cap = n;
   a.overflow = ovf;
-  rep("stencil_emit", timeit([&] { hipLaunchKernelGGL(stencil_emit<3>, dim3((uint32_t)n_tiles), dim3(256), 0, 0, a); }));
+  hipMemset(zero, 0, 4096 * 4);
+  hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3((uint32_t)(n / kStTile)), dim3(256), 0, 0, a);
+  {
+    StencilArgs b = a;
+    b.tile0 = n / kStTile;
+    hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3((uint32_t)(n_tiles - n / kStTile)), dim3(256), 0, 0, b);
+  }
+  rep("stencil_emit", timeit([&] {
+        hipLaunchKernelGGL(stencil_emit<3>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a);
+      }));
+  {
+    uint64_t tt = 0;
+    hipMemcpy(&tt, tot, 8, hipMemcpyDeviceToHost);
+    printf("matches %llu\n", (unsigned long long)tt);
+  }
   rep("mask + emit", timeit([&] {
         hipMemsetAsync(zero, 0, 4096 * 4);
         launch_stencil(3, a, true, 1, 0);

@@ -664,6 +664,31 @@ def test_arrival_order_batch(query):
     assert_parity(g, oracle.run(ir, off, cols, threads=8), off)
 
 
+@pytest.mark.parametrize("query", ["readme", "strict"])
+def test_repeated_batch_allocates_nothing(query):
+    """ A session pushed a batch of the shape it has already seen reuses
+    every device buffer - pools, run queues, the bitmap, the lane order's scratch, the
+    partition's - so a push makes no allocation (an allocation inside a push's timed interval
+    would count its host time, hipFree synchronises, as kernel time), key-partitioned and in
+    arrival order; and the repeated pushes give the same matches."""
+    kind = "abc" if query == "strict" else "stock"
+    cfg = W.SynthConfig("t", kind, 3000, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    keys, acols = W.generate_arrival(cfg)
+    ir = (W.strict_abc_query() if query == "strict" else W.stock_query("readme")).to_ir()
+    s = N.Session(N.Query(ir))
+    s.push(off, cols)
+    first = s.digest(0)
+    assert s.stats(0)["allocs"] > 0
+    for _ in range(3):
+        s.push(off, cols)
+        assert s.stats(0)["allocs"] == 0 and s.digest(0) == first
+    s.push_arrival(keys, acols, cfg.n_keys)
+    for _ in range(3):
+        s.push_arrival(keys, acols, cfg.n_keys)
+        assert s.stats(0)["allocs"] == 0 and s.digest(0) == first
+
+
 def test_arrival_generator_matches_numpy():
     cfg = W.SynthConfig("t", "stock", 300, 200, 77, key_base=5)
     st = N.synth_arrival_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events, cfg.key_base)
