@@ -244,7 +244,7 @@ struct cep_session {
   bool layout_host_valid = false;
   // scratch
   DBuf heavy;  // heavy-key list of the output scatter
-  DBuf rings, walks, nodes, preds, preds0, out, scratch, tile_key, status, keylist, bnd, mask, bhits, retry_rings, bsum;
+  DBuf rings, walks, nodes, preds, preds0, out, scratch, status, keylist, bnd, mask, bhits, retry_rings, bsum;
   DBuf prof;  // measurement runs ($CEP_PROF): the main launch's time split (nfa_lane.h)
   uint32_t last_allocs = 0;  // device allocations the last cep_push_batch made
 };
@@ -305,8 +305,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint32_t m = q->info.arity;
   const uint64_t nk = s->n_keys;
   const uint64_t n_tiles = stencil_tiles(s->n_events);
-  const uint64_t n_groups = n_tiles / 64 + 2;
-  s->tile_key.ensure(sizeof(uint32_t) * (n_tiles + 1));                          // tile counts
+  const uint64_t n_groups = n_tiles / 4 + 2;  // (a count per stencil_emit block: 4 tiles)
   s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
   s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));                     // a match word per 64 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
@@ -359,7 +358,6 @@ void run_stencil(cep_session* s, QueryRt& r) {
   }
   for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
   a.mask = s->mask.as<uint64_t>();
-  a.tile_cnt = s->tile_key.as<uint32_t>();
   a.group_cnt = reinterpret_cast<uint32_t*>(sc + 1);
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();

@@ -16,9 +16,10 @@
 // wave_keys), and a match's key is its word's first key advanced over the key starts.
 //
 // Passes.  (1) stencil_mask streams the column once and writes one 64-bit match word per 64
-// events (1 bit/event), the word's key and sequence number, and a count per tile; (2)
-// stencil_emit sums the counts of the tiles before its own, reads the words back (1/32 of the
-// column's bytes) and writes the matches in order.  No tile waits on another.  (A single pass
+// events (1 bit/event), the word's key and sequence number, and adds each wave's match count to
+// its stencil_emit block's counter; (2) stencil_emit sums the counters of the blocks before its
+// own, reads the words back (1/32 of the column's bytes) and writes the matches in order.  No
+// tile waits on another.  (A single pass
 // with a decoupled look-back over the tile counts was measured slower: 126.7 us against 112.6
 // for the two passes at round 5's start, profiles/r05/ - a tile waits for every tile before
 // it, ~24 look-back round trips deep within one round of co-resident tiles.)
@@ -39,7 +40,6 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int kStThreads = 256;
 constexpr int kStPer = 64;  // events per thread (one 64-bit mask)
 constexpr uint64_t kStTile = (uint64_t)kStThreads * kStPer;
-constexpr uint64_t kStGroup = 64;  // tiles per group count (stencil_emit's offsets)
 
 // ---------------------------------------------------------------- per-batch key index
 constexpr int kStWave = kStTile / (kStThreads / 64);  // 4096 events per wave of stencil_mask
@@ -387,19 +387,31 @@ __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t w
   out.wks = wks;
 }
 
-// Pass 1: per wave the mask phase, its natural words, their keys and sequence numbers, and
-// the match count per tile (and per 64 tiles, for stencil_emit's offsets)
+// stencil_emit's block: kEmW mask tiles; the mask pass counts matches per emit block
+constexpr int kEmW = 4;
+constexpr uint64_t kStGroupChunks = kEmW * (kStTile / kStWave);  // chunks per group count: an emit block's
+
+// Pass 1: per 4096-event chunk (a wave) the mask phase, its natural words, their keys and
+// sequence numbers, and the match count per kStGroupChunks chunks (one stencil_emit block's
+// span: its offset is the sum of the counts before it).  Each wave adds its own count: no
+// block-wide barrier ties four waves together, and a counter takes 16 waves' atomics (probe,
+// profiles/r05/: for 1e8 events the mask phase alone 65.4 us, with the three word stores 76.6,
+// with a block-wide tile count and an atomic per 64 tiles 84.4; an atomic per wave into
+// counters of 256 waves 156).  (A launch of resident waves looping over the chunks, so a
+// chunk's stores overlap the next chunk's loads, measured 142 us: the loop's scalar state spills.)
 // (the full-wave build at 8 waves per SIMD: the scalar registers of the step loop bound its
 // occupancy - 99 SGPRs: 6 waves - and the pass streams better with more waves in flight)
+
 template <int M, bool RANGE, int NCOL, bool FULL>
 __global__ void __launch_bounds__(kStThreads) __attribute__((amdgpu_waves_per_eu(FULL ? 8 : 1)))
 stencil_mask(StencilArgs A) {
-  __shared__ uint32_t s_cnt[kStThreads / 64];
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
   // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t tile = A.tile0 + blockIdx.x;
-  const uint64_t wbase = tile * kStTile + (uint64_t)wv * kStWave;
+  const uint64_t c = (uint64_t)blockIdx.x * (kStThreads / 64) + wv;
+  if (c >= A.n_chunk) return;  // (wave-uniform; no barrier below)
+  const uint64_t chunk = A.chunk0 + c;
+  const uint64_t wbase = chunk * kStWave;
   WaveMask o;
   wave_mask<M, RANGE, NCOL, FULL>(A, wbase, lane, o);
   const uint64_t ws = wbase + (uint64_t)lane * 64;
@@ -410,17 +422,11 @@ stencil_mask(StencilArgs A) {
     A.word_key[ws / 64] = o.wkey | ((o.bw & ~1ull) ? 0x80000000u : 0u);
     A.word_seq[ws / 64] = (uint32_t)(ws - o.wks);
   }
-  // matches of the wave: popcount of each lane's word, summed over the wave once
+  // matches of the chunk: popcount of each lane's word, summed over the wave
   uint32_t cnt = (uint32_t)__popcll(o.nat);
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
-  if (lane == 0) s_cnt[wv] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-    A.tile_cnt[tile] = c;
-    if (c) atomicAdd(A.group_cnt + tile / kStGroup, c);  // per 64 tiles, for stencil_emit
-  }
+  if (lane == 0 && cnt) atomicAdd(A.group_cnt + chunk / kStGroupChunks, cnt);  // (no return value)
 }
 
 // Pass 2: a thread per kEmW consecutive 64-event words (a block: kEmW mask tiles), the block's
@@ -429,7 +435,6 @@ stencil_mask(StencilArgs A) {
 // thread ran 6104 blocks for 1e8 events, three rounds of resident blocks each paying a load
 // and a store round trip: ~18 us; kEmW words per thread issue their loads together and the
 // grid fits the chip in one round.)
-constexpr int kEmW = 4;
 constexpr uint32_t kEmStage = 3072;  // matches staged in LDS (24 KB: 6 blocks per CU)
 
 template <int M>
@@ -466,10 +471,8 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
       ws[i] = v ? A.word_seq[w0 + i] : 0u;
     }
   }
-  uint64_t part = 0;
-  const uint64_t g0 = (t0 / kStGroup) * kStGroup;
-  for (uint64_t i = tid; i < t0 / kStGroup; i += kStThreads) part += A.group_cnt[i];
-  if (g0 + tid < t0) part += A.tile_cnt[g0 + tid];
+  uint64_t part = 0;  // the matches of the blocks before this one: their group counts
+  for (uint64_t i = tid; i < blockIdx.x; i += kStThreads) part += A.group_cnt[i];
   uint32_t cnt = 0;
 #pragma unroll
   for (int i = 0; i < kEmW; i++) cnt += (uint32_t)__popcll(wm[i]);
@@ -578,19 +581,24 @@ static bool range_never(const StencilArgs& a, int m, int ncol) {
 
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
-  // the tiles whose four waves are all whole fast-path waves run the full-wave build, the
-  // rest (the stream's last tile; every tile of an unaligned or interpreted query) the general one
-  const uint64_t full = RANGE && a.aligned && !range_never(a, M, NCOL) ? a.n_events / kStTile : 0;
+  // the whole fast-path chunks run the full-wave build, the rest (the stream's last chunk;
+  // every chunk of an unaligned or interpreted query) the general one
+  const uint64_t n_chunks = (a.n_events + kStWave - 1) / kStWave;
+  const uint64_t full = RANGE && a.aligned && !range_never(a, M, NCOL) ? a.n_events / kStWave : 0;
   StencilArgs b = a;
+  auto blocks = [](uint64_t chunks) { return (uint32_t)((chunks + kStThreads / 64 - 1) / (kStThreads / 64)); };
   if constexpr (RANGE) {
     if (full) {
-      b.tile0 = 0;
-      hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, true>), dim3((uint32_t)full), dim3(kStThreads), 0, st, b);
+      b.chunk0 = 0;
+      b.n_chunk = full;
+      hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, true>), dim3(blocks(full)), dim3(kStThreads), 0,
+                         st, b);
     }
   }
-  if (full < n_tiles) {
-    b.tile0 = full;
-    hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, false>), dim3((uint32_t)(n_tiles - full)), dim3(kStThreads), 0,
+  if (full < n_chunks) {
+    b.chunk0 = full;
+    b.n_chunk = n_chunks - full;
+    hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, false>), dim3(blocks(n_chunks - full)), dim3(kStThreads), 0,
                        st, b);
   }
   hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(kStThreads), 0, st, a);

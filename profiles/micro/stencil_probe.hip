@@ -156,7 +156,7 @@ int main(int argc, char** argv) {
   hipMalloc(&zero, 4096 * 4);
   hipMalloc(&mask, 4 * (n / 256 + 2) * 8);
   hipMalloc(&word_key, 2 * ((n / 64 + 2 + 3) & ~3ull) * 4);
-  hipMalloc(&tile_cnt, (n_tiles + 1) * 4);
+  hipMalloc(&tile_cnt, (n_waves + 1) * 4);
   hipLaunchKernelGGL(gen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, v, n);
   hipLaunchKernelGGL(gen_off, dim3((uint32_t)((n_keys + 256) / 256)), dim3(256), 0, 0, off, n_keys, n);
   launch_wave_keys(off, n_keys, n, wk, zero, 4096, 0);
@@ -176,13 +176,17 @@ int main(int argc, char** argv) {
   a.mask = mask;
   a.word_key = word_key;
   a.word_seq = word_key + ((n / 64 + 2 + 3) & ~3ull);
-  a.tile_cnt = tile_cnt;
   a.group_cnt = zero;
   const double gb = n * 4.0 / 1e9;
   auto rep = [&](const char* name, float us) { printf("%-28s %8.1f us  %5.2f TB/s\n", name, us, gb / (us * 1e-6) / 1e3); };
   rep("rd (16 KB per wave)", timeit([&] { hipLaunchKernelGGL(rd, dim3((uint32_t)n_tiles), dim3(256), 0, 0, (const v4i*)v, n / 4, out); }));
-  rep("stencil_mask (general build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3((uint32_t)n_tiles), dim3(256), 0, 0, a); }));
-  rep("stencil_mask (full-wave build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3((uint32_t)(n / kStTile)), dim3(256), 0, 0, a); }));
+  const uint64_t n_chunks = n_waves, full = n / kStWave;
+  a.chunk0 = 0;
+  a.n_chunk = n_chunks;
+  const uint32_t nb_all = (uint32_t)((n_chunks + 3) / 4), nb_full = (uint32_t)((full + 3) / 4);
+  rep("stencil_mask (general build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3(nb_all), dim3(256), 0, 0, a); }));
+  a.n_chunk = full;
+  rep("stencil_mask (full-wave build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3(nb_full), dim3(256), 0, 0, a); }));
   a.m_key = (uint32_t*)out;  // (probe: the emit pass's outputs, sized for the synthetic stream's matches)
   uint32_t* pseq;
   uint64_t* tot;
@@ -196,12 +200,8 @@ int main(int argc, char** argv) {
   a.out_cap = n;
   a.overflow = ovf;
   hipMemset(zero, 0, 4096 * 4);
-  hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3((uint32_t)(n / kStTile)), dim3(256), 0, 0, a);
-  {
-    StencilArgs b = a;
-    b.tile0 = n / kStTile;
-    hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3((uint32_t)(n_tiles - n / kStTile)), dim3(256), 0, 0, b);
-  }
+  launch_stencil(3, a, true, 1, 0);  // (the counts the emit pass reads)
+  hipDeviceSynchronize();
   rep("stencil_emit", timeit([&] {
         hipLaunchKernelGGL(stencil_emit<3>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a);
       }));
