@@ -72,6 +72,8 @@ struct Tuning {
   bool stream_no_order = false; // $CEP_STREAM_NO_ORDER
   bool no_wm_fold = false;      // $CEP_NO_WM_FOLD: the watermark as its own pass
   bool host_trace = false;      // $CEP_HOST_TRACE: allocations and push phases on stderr
+  int poison_byte = 0xFF;       // $CEP_POISON_BYTE
+  uint64_t poison = 0;          // $CEP_POISON=mask: new device buffers filled with 0xFF (session.cpp DBuf)
 };
 Tuning tuning_from_env();
 // the drain threshold the JIT kernels are compiled with ($CEP_WALK_FLUSH, default 24)
@@ -89,7 +91,9 @@ hipError_t launch_collect_retry(const KeyState* ks, uint64_t n, uint32_t* cap_li
 hipError_t launch_compact(const KeyState* ks, uint64_t n_keys, uint64_t* bsum_m, uint64_t* bsum_p,
                           uint64_t* totals, hipStream_t st);
 uint64_t scatter_heavy_bytes(uint64_t n_keys);
-hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st);  // exclusive, symbol.hip
+// exclusive scan, symbol.hip: `tmp` holds scan_u32_scratch(n) u32 words
+uint64_t scan_u32_scratch(uint64_t n);
+hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp, hipStream_t st);
 hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint32_t* span, const int32_t* status,
                        uint64_t n, uint64_t max_symbols, uint32_t* key, uint64_t* n_symbols, uint32_t* err,
                        hipStream_t st);

@@ -262,11 +262,12 @@ static uint64_t rs_tiles(uint64_t n, int rounds = kRsRounds) {
 
 // Device scratch of lsd_sort: bytes needed for n keys of `bits` bits (histograms and their
 // scan, one (key, value) ping-pong pair per intermediate pass), for the smaller tile.
+// (the histogram scan's own scratch last: no allocation on the sort's path)
 static size_t lsd_scratch_bytes(uint64_t n, int bits) {
   const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
   const uint64_t h = (uint64_t)(1u << kRsMaxBits) * rs_tiles(n, kRsRoundsMin);
   const uint64_t mid = passes > 1 ? (uint64_t)(passes > 2 ? 2 : 1) * 8 * std::max<uint64_t>(n, 1) : 0;
-  return 4 * (2 * h + 256) + mid + 1024;
+  return 4 * (2 * h + 256) + mid + 4 * scan_u32_scratch(h) + 1024;
 }
 
 // Stable sort of n u32 keys (`bits` significant bits; inv: by ~key, i.e. descending) ->
@@ -286,6 +287,8 @@ static hipError_t lsd_sort_r(const uint32_t* key, uint64_t n, int bits, bool inv
   // (the ping-pong pairs sit past the smaller tile's histograms: the same place for either tile)
   uint32_t* mid = (uint32_t*)((char*)scratch + 4 * (2 * (uint64_t)(1u << kRsMaxBits) * rs_tiles(n, kRsRoundsMin) + 256));
   uint32_t *mk[2] = {mid, mid + 2 * n}, *mv[2] = {mid + n, mid + 3 * n};
+  const uint64_t mid_words = passes > 1 ? (uint64_t)(passes > 2 ? 2 : 1) * 2 * std::max<uint64_t>(n, 1) : 0;
+  uint32_t* stmp = mid + mid_words;  // (lsd_scratch_bytes: the scan's scratch after the pairs)
   const uint32_t *ik = key, *iv = nullptr;
   const dim3 g((uint32_t)T), gh((uint32_t)((T + kRsHistTiles - 1) / kRsHistTiles)), b(kRsThreads);
   hipError_t e = hipSuccess;
@@ -298,7 +301,7 @@ static hipError_t lsd_sort_r(const uint32_t* key, uint64_t n, int bits, bool inv
     if (p > 0) hipLaunchKernelGGL((rs_hist<false, false, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
     else if (inv) hipLaunchKernelGGL((rs_hist<true, true, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
     else hipLaunchKernelGGL((rs_hist<true, false, R>), gh, b, 0, st, ik, n, nk, shift, w, hist, T, bad);
-    if ((e = scan_u32(hist, hoff, ((uint64_t)1 << w) * T, st)) != hipSuccess) return e;
+    if ((e = scan_u32(hist, hoff, ((uint64_t)1 << w) * T, stmp, st)) != hipSuccess) return e;
     if (p > 0) hipLaunchKernelGGL((rs_scatter<false, false, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
     else if (inv) hipLaunchKernelGGL((rs_scatter<true, true, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);
     else hipLaunchKernelGGL((rs_scatter<true, false, R>), g, b, 0, st, ik, iv, n, shift, w, hoff, T, ok, ov);

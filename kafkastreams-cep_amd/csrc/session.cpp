@@ -49,6 +49,16 @@ static bool g_host_trace = false;
 static bool host_trace() { return g_host_trace; }
 // device allocations made (DBuf ensure / grow_keep): cep_batch_stats.allocs counts a batch's
 static thread_local uint32_t g_allocs = 0;
+// $CEP_POISON=mask (measurement runs): the session's k-th device allocation (k < 64, bit k of
+// the mask; -1: all) filled with 0xFF bytes (CEP_NONE words; $CEP_POISON_BYTE another byte), so a read of memory no kernel wrote is not hidden
+// by a fresh allocation's zeros
+static uint64_t g_poison = 0;
+static uint32_t g_poison_base = 0;
+static int g_poison_byte = 0xFF;  // ($CEP_POISON_BYTE)
+static bool poison_next() {
+  const uint32_t k = g_allocs - g_poison_base;
+  return k < 64 && ((g_poison >> k) & 1u);
+}
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -69,11 +79,17 @@ struct DBuf {
     if (p) HIPCHECK(hipFree(p));
     p = nullptr;
     bytes = 0;
+    const bool poison = poison_next();
+    if (host_trace()) std::fprintf(stderr, "cep_host alloc #%u\n", g_allocs - g_poison_base);
     g_allocs++;
     n = std::max<size_t>(n, 256);
     if (hipMalloc(&p, n) != hipSuccess) {
       p = nullptr;
       throw std::bad_alloc();
+    }
+    if (poison) {  // (synchronous: the null stream does not order with the session's)
+      HIPCHECK(hipMemset(p, g_poison_byte, n));
+      HIPCHECK(hipDeviceSynchronize());
     }
     bytes = n;
   }
@@ -89,8 +105,13 @@ struct DBuf {
       }
     } tr{t0, n};
     void* q = nullptr;
+    const bool poison = poison_next();
     g_allocs++;
     if (hipMalloc(&q, n) != hipSuccess) throw std::bad_alloc();
+    if (poison) {
+      HIPCHECK(hipMemset(q, g_poison_byte, n));
+      HIPCHECK(hipDeviceSynchronize());
+    }
     if (p && keep) HIPCHECK(hipMemcpyAsync(q, p, std::min(keep, bytes), hipMemcpyDeviceToDevice, st));
     HIPCHECK(hipStreamSynchronize(st));
     if (p) HIPCHECK(hipFree(p));
@@ -244,7 +265,7 @@ struct cep_session {
   bool layout_host_valid = false;
   // scratch
   DBuf heavy;  // heavy-key list of the output scatter
-  DBuf rings, walks, nodes, preds, preds0, out, scratch, status, keylist, bnd, mask, bhits, retry_rings, bsum;
+  DBuf rings, walks, nodes, preds, preds0, out, scratch, status, keylist, mask, bhits, retry_rings, bsum;
   DBuf prof;  // measurement runs ($CEP_PROF): the main launch's time split (nfa_lane.h)
   uint32_t last_allocs = 0;  // device allocations the last cep_push_batch made
 };
@@ -307,10 +328,8 @@ void run_stencil(cep_session* s, QueryRt& r) {
   const uint64_t n_tiles = stencil_tiles(s->n_events);
   const uint64_t n_groups = n_tiles / 4 + 2;  // (a count per stencil_emit block: 4 tiles)
   s->status.ensure(sizeof(Scratch) + sizeof(uint32_t) * n_groups);               // counters + group counts
-  s->mask.ensure(sizeof(uint64_t) * (s->n_events / 64 + 2));                     // a match word per 64 events
+  s->mask.ensure(16 * (s->n_events / 64 + 2));                                   // a 16-B record per 64 events
   s->keylist.ensure(sizeof(uint32_t) * (stencil_waves(s->n_events) + 1));        // wave -> key
-  const uint64_t nw4 = (s->n_events / 64 + 2 + 3) & ~3ull;  // (word_seq 16-B aligned: stencil_emit's loads)
-  s->bnd.ensure(sizeof(uint32_t) * 2 * nw4);                                     // word -> key, sequence number
   // worst case one match per event
   const uint64_t cap = std::max<uint64_t>(s->n_events, 1);
   if (!r.h_sc) {
@@ -340,8 +359,6 @@ void run_stencil(cep_session* s, QueryRt& r) {
   a.n_events = s->n_events;
   a.key_off = s->key_off;
   a.wave_key = s->keylist.as<uint32_t>();
-  a.word_key = s->bnd.as<uint32_t>();
-  a.word_seq = a.word_key + nw4;
   a.q = r.d_q.as<DevQuery>();
   a.code = r.d_code.as<uint32_t>();
   a.cols = s->cols;
@@ -357,7 +374,7 @@ void run_stencil(cep_session* s, QueryRt& r) {
     }
   }
   for (uint32_t x = 0; x < m && x < (uint32_t)kMaxStencil; x++) a.stage_name[x] = q->arityStage[x];
-  a.mask = s->mask.as<uint64_t>();
+  a.words = s->mask.as<uint4>();
   a.group_cnt = reinterpret_cast<uint32_t*>(sc + 1);
   a.m_key = r.m_key.as<uint32_t>();
   a.p_seq = r.p_seq.as<uint32_t>();
@@ -985,6 +1002,9 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
   if (opts) s->opts = *opts;
   s->tune = cep::tuning_from_env();  // (the only read of the measurement knobs: not per launch)
   if (s->tune.host_trace) g_host_trace = true;
+  g_poison = s->tune.poison;
+  g_poison_byte = s->tune.poison_byte;
+  g_poison_base = g_allocs;
   for (int i = 0; i < n_queries; i++)
     if (queries[i]->windowed && s->opts.tier != CEP_TIER_JIT)
       return fail(CEP_E_INVALID, "semantic WITHIN runs on the JIT tier only");

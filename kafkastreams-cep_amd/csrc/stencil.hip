@@ -188,14 +188,11 @@ struct WaveMask {
 // windows crossing a key start are settled after the loop, on the natural words, with vector
 // work.  (This keeps the loop's scalar registers down - 58 instead of 106, 8 waves per SIMD
 // instead of 6 - and the pass at ~75 us for 1e8 events instead of ~90: profiles/r05/.)
-// FULL: the launch holds whole waves of the range fast path only (aligned columns, no empty
-// range: run_stencil's full tiles) - the slow path's code and its registers are compiled out
-template <int M, bool RANGE, int NCOL, bool FULL>
+template <int M, bool RANGE, int NCOL>
 __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t wbase, const int lane, WaveMask& out) {
-  static_assert(!FULL || RANGE, "the full-wave build is the range fast path");
   constexpr int H = M - 1;              // events a window reaches back
   const StEval<M, RANGE, NCOL> ev(A);
-  const bool fast = FULL || (RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never);
+  const bool fast = RANGE && A.aligned && wbase + kStWave <= A.n_events && !ev.never;
   // The fast path's first step is requested before anything else: the key-start words and
   // the seed events below are dependent round trips
   const v4i* c0 = reinterpret_cast<const v4i*>(A.col[0] + wbase) + lane;
@@ -339,7 +336,7 @@ __device__ __forceinline__ void wave_mask(const StencilArgs& A, const uint64_t w
       ya = NCOL > 1 ? __builtin_nontemporal_load(c1 + qn * 64) : xa;
       step(q + 1, xb, yb, std::true_type{});
     }
-  } else if constexpr (!FULL) {
+  } else {
     const v4i z = {0, 0, 0, 0};
     for (int q = 0; q < kStSteps; q++) step(q, z, z, std::false_type{});
   }
@@ -399,29 +396,23 @@ constexpr uint64_t kStGroupChunks = kEmW * (kStTile / kStWave);  // chunks per g
 // with a block-wide tile count and an atomic per 64 tiles 84.4; an atomic per wave into
 // counters of 256 waves 156).  (A launch of resident waves looping over the chunks, so a
 // chunk's stores overlap the next chunk's loads, measured 142 us: the loop's scalar state spills.)
-// (the full-wave build at 8 waves per SIMD: the scalar registers of the step loop bound its
-// occupancy - 99 SGPRs: 6 waves - and the pass streams better with more waves in flight)
 
-template <int M, bool RANGE, int NCOL, bool FULL>
-__global__ void __launch_bounds__(kStThreads) __attribute__((amdgpu_waves_per_eu(FULL ? 8 : 1)))
-stencil_mask(StencilArgs A) {
+template <int M, bool RANGE, int NCOL>
+__global__ void __launch_bounds__(kStThreads) stencil_mask(StencilArgs A) {
   // wv through readfirstlane: the compiler cannot see that threadIdx.x >> 6 is wave-uniform,
   // and everything derived from it (the fast-path branch, the ballot words) would go to VGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t c = (uint64_t)blockIdx.x * (kStThreads / 64) + wv;
-  if (c >= A.n_chunk) return;  // (wave-uniform; no barrier below)
-  const uint64_t chunk = A.chunk0 + c;
+  const uint64_t chunk = (uint64_t)blockIdx.x * (kStThreads / 64) + wv;
+  if (chunk >= A.n_chunk) return;  // (wave-uniform; no barrier below)
   const uint64_t wbase = chunk * kStWave;
   WaveMask o;
-  wave_mask<M, RANGE, NCOL, FULL>(A, wbase, lane, o);
+  wave_mask<M, RANGE, NCOL>(A, wbase, lane, o);
   const uint64_t ws = wbase + (uint64_t)lane * 64;
   // (bit 31: a key starts inside the word after its first event - stencil_emit walks key_off
   // there; elsewhere a match's sequence number is word_seq + its offset in the word)
-  if (ws < A.n_events) {
-    A.mask[ws / 64] = o.nat;
-    A.word_key[ws / 64] = o.wkey | ((o.bw & ~1ull) ? 0x80000000u : 0u);
-    A.word_seq[ws / 64] = (uint32_t)(ws - o.wks);
-  }
+  if (ws < A.n_events)  // one 16-B store per word (three separate word arrays cost 2-3 us more)
+    A.words[ws / 64] = uint4{(uint32_t)o.nat, (uint32_t)(o.nat >> 32), o.wkey | ((o.bw & ~1ull) ? 0x80000000u : 0u),
+                             (uint32_t)(ws - o.wks)};
   // matches of the chunk: popcount of each lane's word, summed over the wave
   uint32_t cnt = (uint32_t)__popcll(o.nat);
 #pragma unroll
@@ -431,7 +422,7 @@ stencil_mask(StencilArgs A) {
 
 // Pass 2: a thread per kEmW consecutive 64-event words (a block: kEmW mask tiles), the block's
 // offset from the group and tile counts, a block scan for the threads' offsets.  A match's key
-// is its word's first key (word_key) advanced over the key offsets it passes.  (One word per
+// is its word's first key advanced over the key offsets it passes.  (One word per
 // thread ran 6104 blocks for 1e8 events, three rounds of resident blocks each paying a load
 // and a store round trip: ~18 us; kEmW words per thread issue their loads together and the
 // grid fits the chip in one round.)
@@ -446,30 +437,16 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
   const uint64_t t0 = (uint64_t)blockIdx.x * kEmW;  // the block's first mask tile
   const uint64_t n_words = (A.n_events + 63) / 64;
   const uint64_t w0 = t0 * (kStTile / 64) + (uint64_t)tid * kEmW;  // this thread's first word
-  // Every independent load is issued before the first use: the thread's words (16-B loads:
-  // kEmW is 4, the word index a multiple of 4), their first keys and sequence numbers, and the
-  // counts of the tiles before the block (its offset).
+  // Every independent load is issued before the first use: the thread's words (a 16-B record
+  // each: match bits, first key, sequence number) and the counts of the blocks before this one.
   uint64_t wm[kEmW];
   uint32_t wk[kEmW], ws[kEmW];
-  if (w0 + kEmW <= n_words) {
-    const uint4 m01 = *reinterpret_cast<const uint4*>(A.mask + w0);
-    const uint4 m23 = *reinterpret_cast<const uint4*>(A.mask + w0 + 2);
-    const uint4 k4 = *reinterpret_cast<const uint4*>(A.word_key + w0);
-    const uint4 s4 = *reinterpret_cast<const uint4*>(A.word_seq + w0);
-    wm[0] = ((uint64_t)m01.y << 32) | m01.x;
-    wm[1] = ((uint64_t)m01.w << 32) | m01.z;
-    wm[2] = ((uint64_t)m23.y << 32) | m23.x;
-    wm[3] = ((uint64_t)m23.w << 32) | m23.z;
-    wk[0] = k4.x, wk[1] = k4.y, wk[2] = k4.z, wk[3] = k4.w;
-    ws[0] = s4.x, ws[1] = s4.y, ws[2] = s4.z, ws[3] = s4.w;
-  } else {
 #pragma unroll
-    for (int i = 0; i < kEmW; i++) {
-      const bool v = w0 + i < n_words;
-      wm[i] = v ? A.mask[w0 + i] : 0ull;
-      wk[i] = v ? A.word_key[w0 + i] : 0u;
-      ws[i] = v ? A.word_seq[w0 + i] : 0u;
-    }
+  for (int i = 0; i < kEmW; i++) {
+    const uint4 x = w0 + i < n_words ? A.words[w0 + i] : uint4{0, 0, 0, 0};
+    wm[i] = ((uint64_t)x.y << 32) | x.x;
+    wk[i] = x.z;
+    ws[i] = x.w;
   }
   uint64_t part = 0;  // the matches of the blocks before this one: their group counts
   for (uint64_t i = tid; i < blockIdx.x; i += kStThreads) part += A.group_cnt[i];
@@ -571,36 +548,13 @@ hipError_t launch_wave_keys(const uint64_t* key_off, uint64_t n_keys, uint64_t n
 
 uint64_t stencil_waves(uint64_t n_events) { return (n_events + kStWave - 1) / kStWave; }
 
-// an empty stage range: no event can be in that stage (StEval::never, the slow path's case)
-static bool range_never(const StencilArgs& a, int m, int ncol) {
-  for (int s = 0; s < m; s++)
-    for (int c = 0; c < ncol; c++)
-      if (a.rs[s].lo[c] > a.rs[s].hi[c] || a.rs[s].lo[c] > INT32_MAX || a.rs[s].hi[c] < INT32_MIN) return true;
-  return false;
-}
-
 template <int M, bool RANGE, int NCOL>
 static hipError_t launch_one(const StencilArgs& a, uint64_t n_tiles, hipStream_t st) {
-  // the whole fast-path chunks run the full-wave build, the rest (the stream's last chunk;
-  // every chunk of an unaligned or interpreted query) the general one
-  const uint64_t n_chunks = (a.n_events + kStWave - 1) / kStWave;
-  const uint64_t full = RANGE && a.aligned && !range_never(a, M, NCOL) ? a.n_events / kStWave : 0;
+  // (a separate build for the whole fast-path chunks, without the slow path's code and
+  // registers, measured the same - 79.5 against 79.6 us for 1e8 events - and cost a launch)
   StencilArgs b = a;
-  auto blocks = [](uint64_t chunks) { return (uint32_t)((chunks + kStThreads / 64 - 1) / (kStThreads / 64)); };
-  if constexpr (RANGE) {
-    if (full) {
-      b.chunk0 = 0;
-      b.n_chunk = full;
-      hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, true>), dim3(blocks(full)), dim3(kStThreads), 0,
-                         st, b);
-    }
-  }
-  if (full < n_chunks) {
-    b.chunk0 = full;
-    b.n_chunk = n_chunks - full;
-    hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL, false>), dim3(blocks(n_chunks - full)), dim3(kStThreads), 0,
-                       st, b);
-  }
+  b.n_chunk = (a.n_events + kStWave - 1) / kStWave;
+  hipLaunchKernelGGL((stencil_mask<M, RANGE, NCOL>), dim3((uint32_t)((b.n_chunk + 3) / 4)), dim3(kStThreads), 0, st, b);
   hipLaunchKernelGGL(stencil_emit<M>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(kStThreads), 0, st, a);
   return hipGetLastError();
 }

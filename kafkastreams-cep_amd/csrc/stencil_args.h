@@ -23,13 +23,12 @@ struct StencilArgs {
   uint16_t prog[kMaxStencil];
   uint16_t stage_name[kMaxStencil];    // walk order: stage name of pair t (t = 0 is the final event)
   bool aligned;              // col[] 16-B aligned: vector loads
-  uint64_t chunk0, n_chunk;  // stencil_mask: the launch's first kStWave-event chunk, its chunks
-                             // (the full-wave and general builds)
+  uint64_t n_chunk;          // stencil_mask: kStWave-event chunks (one a wave)
   // pass 1 -> pass 3
-  uint64_t* mask;            // per 64 events a word: bit i = a match ends at event 64 w + i
-  uint32_t* word_key;        // key holding event 64 w, for every 64-event word w (pass 1); bit 31: a key
-                             // starts inside the word after its first event
-  uint32_t* word_seq;        // event 64 w's sequence number within that key (pass 1)
+  // per 64-event word w (pass 1): {match bits lo, hi (bit i: a match ends at event 64 w + i), the
+  // key holding event 64 w (bit 31: a key starts inside the word after its first event), event
+  // 64 w's sequence number within that key}
+  uint4* words;
   uint32_t* group_cnt;       // matches per stencil_emit block's span (pass 1, atomics; zeroed per batch)
   // output
   uint32_t* m_key;

@@ -248,22 +248,24 @@ __global__ void __launch_bounds__(256) sym_assign(const uint8_t* __restrict__ by
 
 }  // namespace
 
+// u32 words of scratch scan_u32 needs for n values: the tile sums and their scan, per level
+uint64_t scan_u32_scratch(uint64_t n) {
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  return tiles <= 1 ? tiles * 2 : 2 * tiles + scan_u32_scratch(tiles);
+}
+
 // exclusive scan of n u32 (in -> out, n < 2^32 and the total too), recursing over the tile
-// sums; shared with the partition (cep_internal.h)
-hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t st) {
+// sums in `tmp` (scan_u32_scratch(n) words); shared with the partition (cep_internal.h)
+hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t* tmp, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-  uint32_t *sums = nullptr, *pre = nullptr;
-  hipError_t e = hipMallocAsync((void**)&sums, 4 * tiles, st);
-  if (e != hipSuccess) return e;
-  if ((e = hipMallocAsync((void**)&pre, 4 * tiles, st)) != hipSuccess) return e;
+  uint32_t *sums = tmp, *pre = tmp + tiles;
   hipLaunchKernelGGL(scan_tiles, dim3((uint32_t)tiles), dim3(kScanBlock), 0, st, in, n, out, sums);
   if (tiles > 1) {
-    if ((e = scan_u32(sums, pre, tiles, st)) != hipSuccess) return e;
+    hipError_t e = scan_u32(sums, pre, tiles, tmp + 2 * tiles, st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(scan_add, dim3((uint32_t)tiles), dim3(kScanBlock), 0, st, out, n, pre);
   }
-  (void)hipFreeAsync(sums, st);
-  (void)hipFreeAsync(pre, st);
   return hipGetLastError();
 }
 
@@ -277,19 +279,20 @@ hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint
   const uint64_t want = 2 * (max_symbols < n ? max_symbols : n);
   while (cap < want) cap <<= 1;
   unsigned long long* tab_hash = nullptr;
-  uint32_t *tab_rep = nullptr, *slot_of = nullptr, *first = nullptr, *prefix = nullptr, *err = nullptr;
+  uint32_t *tab_rep = nullptr, *slot_of = nullptr, *first = nullptr, *prefix = nullptr, *err = nullptr, *stmp = nullptr;
   hipError_t e = hipSuccess;
   auto ok = [&](hipError_t x) { if (e == hipSuccess) e = x; return e == hipSuccess; };
   if (ok(hipMallocAsync((void**)&tab_hash, 8 * cap, st)) && ok(hipMallocAsync((void**)&tab_rep, 4 * cap, st)) &&
       ok(hipMallocAsync((void**)&slot_of, 4 * n, st)) && ok(hipMallocAsync((void**)&first, 4 * n, st)) &&
       ok(hipMallocAsync((void**)&prefix, 4 * (n + 1), st)) && ok(hipMallocAsync((void**)&err, 4, st)) &&
+      ok(hipMallocAsync((void**)&stmp, 4 * (scan_u32_scratch(n) + 1), st)) &&
       ok(hipMemsetAsync(tab_hash, 0, 8 * cap, st)) && ok(hipMemsetAsync(tab_rep, 0xFF, 4 * cap, st)) &&
       ok(hipMemsetAsync(err, 0, 4, st))) {
     const dim3 g((uint32_t)((n + 255) / 256));
     hipLaunchKernelGGL(sym_insert, g, dim3(256), 0, st, bytes, rec_off, span, status, n, tab_hash, tab_rep, cap - 1,
                        slot_of, err);
     hipLaunchKernelGGL(sym_first, g, dim3(256), 0, st, slot_of, tab_rep, n, first);
-    if (ok(scan_u32(first, prefix, n, st))) {
+    if (ok(scan_u32(first, prefix, n, stmp, st))) {
       hipLaunchKernelGGL(sym_assign, g, dim3(256), 0, st, bytes, rec_off, span, slot_of, tab_rep, prefix, n, key, err);
       uint32_t last[2] = {0, 0};
       if (ok(hipGetLastError()) && ok(hipMemcpyAsync(&last[0], prefix + n - 1, 4, hipMemcpyDeviceToHost, st)) &&
@@ -298,7 +301,7 @@ hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint
         *n_symbols = (uint64_t)last[0] + last[1];
     }
   }
-  for (void* p : {(void*)tab_hash, (void*)tab_rep, (void*)slot_of, (void*)first, (void*)prefix, (void*)err})
+  for (void* p : {(void*)tab_hash, (void*)tab_rep, (void*)slot_of, (void*)first, (void*)prefix, (void*)err, (void*)stmp})
     if (p) (void)hipFreeAsync(p, st);
   (void)hipStreamSynchronize(st);
   return e;

@@ -50,6 +50,8 @@ Tuning tuning_from_env() {
   t.stream_no_order = flag("CEP_STREAM_NO_ORDER");
   t.no_wm_fold = flag("CEP_NO_WM_FOLD");
   t.host_trace = flag("CEP_HOST_TRACE");
+  if (const char* v = std::getenv("CEP_POISON")) t.poison = std::strtoull(v, nullptr, 0);
+  t.poison_byte = (int)num("CEP_POISON_BYTE", 0xFF);
   return t;
 }
 #else

@@ -154,7 +154,7 @@ int main(int argc, char** argv) {
   const uint64_t n_waves = stencil_waves(n), n_tiles = stencil_tiles(n);
   hipMalloc(&wk, (n_waves + 1) * 4);
   hipMalloc(&zero, 4096 * 4);
-  hipMalloc(&mask, 4 * (n / 256 + 2) * 8);
+  hipMalloc(&mask, 16 * (n / 64 + 2));
   hipMalloc(&word_key, 2 * ((n / 64 + 2 + 3) & ~3ull) * 4);
   hipMalloc(&tile_cnt, (n_waves + 1) * 4);
   hipLaunchKernelGGL(gen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, v, n);
@@ -173,20 +173,15 @@ int main(int argc, char** argv) {
     a.rs[s].lo[0] = a.rs[s].lo[1] = lo[s];
     a.rs[s].hi[0] = a.rs[s].hi[1] = hi[s];
   }
-  a.mask = mask;
-  a.word_key = word_key;
-  a.word_seq = word_key + ((n / 64 + 2 + 3) & ~3ull);
+  a.words = reinterpret_cast<uint4*>(mask);
   a.group_cnt = zero;
   const double gb = n * 4.0 / 1e9;
   auto rep = [&](const char* name, float us) { printf("%-28s %8.1f us  %5.2f TB/s\n", name, us, gb / (us * 1e-6) / 1e3); };
   rep("rd (16 KB per wave)", timeit([&] { hipLaunchKernelGGL(rd, dim3((uint32_t)n_tiles), dim3(256), 0, 0, (const v4i*)v, n / 4, out); }));
-  const uint64_t n_chunks = n_waves, full = n / kStWave;
-  a.chunk0 = 0;
+  const uint64_t n_chunks = n_waves;
   a.n_chunk = n_chunks;
-  const uint32_t nb_all = (uint32_t)((n_chunks + 3) / 4), nb_full = (uint32_t)((full + 3) / 4);
-  rep("stencil_mask (general build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, false>), dim3(nb_all), dim3(256), 0, 0, a); }));
-  a.n_chunk = full;
-  rep("stencil_mask (full-wave build)", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1, true>), dim3(nb_full), dim3(256), 0, 0, a); }));
+  const uint32_t nb_all = (uint32_t)((n_chunks + 3) / 4);
+  rep("stencil_mask", timeit([&] { hipLaunchKernelGGL((stencil_mask<3, true, 1>), dim3(nb_all), dim3(256), 0, 0, a); }));
   a.m_key = (uint32_t*)out;  // (probe: the emit pass's outputs, sized for the synthetic stream's matches)
   uint32_t* pseq;
   uint64_t* tot;

@@ -3,6 +3,7 @@
 Bit-exact on every array: match keys, emission events, walk pairs (stage, event) in
 reference order, per-key exception class and position, and the device checksum.
 """
+import json
 import os
 
 import numpy as np
@@ -680,13 +681,28 @@ def test_repeated_batch_allocates_nothing(query):
     s.push(off, cols)
     first = s.digest(0)
     assert s.stats(0)["allocs"] > 0
+    seen = []  # (push kind, stats, digest): the whole history in a failure's message
+
+    def check(kind):
+        seen.append((kind, s.stats(0), s.digest(0)))
+        if seen[-1][1]["allocs"] or seen[-1][2] != first:
+            diag = {}
+            if kind == "arrival":  # was the partition right?
+                ko, perm, _ = s.layout()
+                diag["key_off_equal"] = bool(np.array_equal(ko, off))
+                if perm is not None:
+                    pk = keys[perm.astype(np.int64)]
+                    diag["perm_keys_sorted"] = bool(np.all(np.diff(pk.astype(np.int64)) >= 0))
+                    diag["perm_stable"] = bool(np.all((np.diff(perm.astype(np.int64)) > 0) | (np.diff(pk.astype(np.int64)) > 0)))
+            pytest.fail(json.dumps({"pushes": seen, "diag": diag}))
     for _ in range(3):
         s.push(off, cols)
-        assert s.stats(0)["allocs"] == 0 and s.digest(0) == first
+        check("csr")
     s.push_arrival(keys, acols, cfg.n_keys)
-    for _ in range(3):
+    seen.append(("arrival first", s.stats(0), s.digest(0)))
+    for _ in range(6):
         s.push_arrival(keys, acols, cfg.n_keys)
-        assert s.stats(0)["allocs"] == 0 and s.digest(0) == first
+        check("arrival")
 
 
 def test_arrival_generator_matches_numpy():
