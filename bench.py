@@ -419,10 +419,46 @@ def processor_throughput(device, n_keys=10_000, per_key=100, batch=65_536):
         ctx.send(k, v, ts)
     proc.close()
     el = time.perf_counter() - t0
-    return {"workload": f"CEPProcessor.process() per record, README query, {n_keys} keys x {per_key} records "
-                        f"(round-robin arrival), batch {batch}, in_memory", "value": len(recs) / el,
-            "unit": "records/s", "records": len(recs), "forwarded": len(ctx.forwarded),
-            "matches_per_s": len(ctx.forwarded) / el, "seconds": el}
+    res = {"workload": f"CEPProcessor.process() per record, README query, {n_keys} keys x {per_key} records "
+                       f"(round-robin arrival), batch {batch}, in_memory", "value": len(recs) / el,
+           "unit": "records/s", "records": len(recs), "forwarded": len(ctx.forwarded),
+           "matches_per_s": len(ctx.forwarded) / el, "seconds": el}
+    res["latency"] = processor_latency(device, recs, n_keys)
+    return res
+
+
+def processor_latency(device, recs, n_keys, batch=None):
+    """ Time from process() to forward at the processor's default batch
+    size: a record is forwarded by the flush of the batch it lands in, so the newest record of a
+    batch waits that flush (the GPU push, the match read-back and the Sequence forwarding) and
+    the oldest the batch's fill time before it too.  Per flush: its wall time and the fill time
+    since the previous flush ended."""
+    from kafkastreams_cep_amd import processor as P
+    ctx = P.RecordContext("StockEvents", 0)
+    kw = {} if batch is None else {"batch_size": batch}
+    proc = P.CEPProcessor(W.stock_query("readme"), in_memory=True, max_keys=n_keys, device=device, **kw)
+    proc.init(ctx)
+    flush_ms, fill_ms = [], []
+    orig = proc.flush
+    last = [time.perf_counter()]
+
+    def timed_flush():
+        t = time.perf_counter()
+        orig()
+        e = time.perf_counter()
+        flush_ms.append(1e3 * (e - t))
+        fill_ms.append(1e3 * (t - last[0]))
+        last[0] = e
+    proc.flush = timed_flush
+    for k, v, ts in recs:
+        ctx.send(k, v, ts)
+    proc.close()
+    f, g = np.array(flush_ms[:-1] or flush_ms), np.array(fill_ms[:-1] or fill_ms)  # (the last: close's partial batch)
+    return {"batch_size": proc.batch_size, "flushes": len(flush_ms),
+            "flush_ms_mean": float(f.mean()), "flush_ms_p99": float(np.percentile(f, 99)),
+            "fill_ms_mean": float(g.mean()),
+            "newest_record_ms": float(f.mean()), "oldest_record_ms": float((f + g).mean()),
+            "note": "per record, process() to forward: between the newest (flush only) and the oldest (fill + flush) of its batch"}
 
 
 def projected_scaling(device, cfg, stream, world, steps, dist, t1_ms=None):

@@ -176,6 +176,30 @@ def test_cfg3_medium_bit_exact():
     assert_parity(gpu_run(ir, off, cols), r, off)
 
 
+def test_cfg3_streaming_medium_bit_exact():
+    """ The streaming path the processor runs, at scale against the oracle
+    instead of the GPU's own per-batch checksum: config 3 at 20k keys (every 50th key of the
+    BASELINE stream, 20M events) cut into 10 consecutive batches per key at random points - every
+    key's matches (global sequence numbers, emission order, stage names) and exceptions equal
+    the oracle's single pass (the stream build, its carried run queues and pools, the lane
+    order blended across batches)."""
+    import stream_split as SS
+    cfg = W.CONFIGS[3]
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 50))
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=16)
+    assert r["n_matches"] > 10000
+    s = N.Session(N.Query(ir), streaming=True)
+    outs = []
+    for ko, cs in SS.split(off, cols, 10, seed=10):
+        s.push(ko, cs)
+        m = s.matches(0)
+        m["err_code"], m["err_seq"] = s.key_errors(0)
+        outs.append(m)
+    assert SS.merge(outs) == SS.oracle_per_key(r, off)
+    np.testing.assert_array_equal(outs[-1]["err_code"], r["err_code"])
+
+
 def test_cfg4_stress_medium_bit_exact():
     """Config 4's stress variant at 20k keys (20M events, ~200 buffer nodes per key)."""
     cfg = W.CONFIGS[3]
