@@ -449,7 +449,13 @@ __global__ void __launch_bounds__(kStThreads) stencil_emit(StencilArgs A) {
     ws[i] = x.w;
   }
   uint64_t part = 0;  // the matches of the blocks before this one: their group counts
-  for (uint64_t i = tid; i < blockIdx.x; i += kStThreads) part += A.group_cnt[i];
+  // (the first 8 per thread issued together: a late block of 1e8 events has ~1500 before it)
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)r * kStThreads;
+    part += i < blockIdx.x ? A.group_cnt[i] : 0u;
+  }
+  for (uint64_t i = (uint64_t)tid + 8 * kStThreads; i < blockIdx.x; i += kStThreads) part += A.group_cnt[i];
   uint32_t cnt = 0;
 #pragma unroll
   for (int i = 0; i < kEmW; i++) cnt += (uint32_t)__popcll(wm[i]);

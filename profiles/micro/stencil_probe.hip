@@ -124,6 +124,124 @@ __global__ void __launch_bounds__(256) v2(StencilArgs A, uint64_t* out) {
   out[(wbase / 64) % (1u << 20) + lane] = myword ^ wkey;
 }
 
+// emit ablation (probe): ABL 0 loads + scans only, 1 + LDS staging, 2 = stencil_emit
+template <int M, int ABL>
+__global__ void __launch_bounds__(kStThreads) emit_abl(StencilArgs A) {
+  __shared__ uint32_t s_wsum[kStThreads / 64];
+  __shared__ uint64_t s_toff[kStThreads / 64];
+  __shared__ uint2 s_stage[kEmStage];  // (key, sequence number of the final event)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kEmW;  // the block's first mask tile
+  const uint64_t n_words = (A.n_events + 63) / 64;
+  const uint64_t w0 = t0 * (kStTile / 64) + (uint64_t)tid * kEmW;  // this thread's first word
+  // Every independent load is issued before the first use: the thread's words (a 16-B record
+  // each: match bits, first key, sequence number) and the counts of the blocks before this one.
+  uint64_t wm[kEmW];
+  uint32_t wk[kEmW], ws[kEmW];
+#pragma unroll
+  for (int i = 0; i < kEmW; i++) {
+    const uint4 x = w0 + i < n_words ? A.words[w0 + i] : uint4{0, 0, 0, 0};
+    wm[i] = ((uint64_t)x.y << 32) | x.x;
+    wk[i] = x.z;
+    ws[i] = x.w;
+  }
+  uint64_t part = 0;  // the matches of the blocks before this one: their group counts
+  // (the first 8 per thread issued together: a late block of 1e8 events has ~1500 before it)
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)r * kStThreads;
+    part += i < blockIdx.x ? A.group_cnt[i] : 0u;
+  }
+  for (uint64_t i = (uint64_t)tid + 8 * kStThreads; i < blockIdx.x; i += kStThreads) part += A.group_cnt[i];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < kEmW; i++) cnt += (uint32_t)__popcll(wm[i]);
+  // block exclusive scan of the threads' match counts
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_down(part, off, 64);
+  if (lane == 63) s_wsum[wv] = incl;
+  if (lane == 0) s_toff[wv] = part;
+  __syncthreads();
+  uint32_t woff = 0;
+#pragma unroll
+  for (int w = 0; w < kStThreads / 64; w++)
+    if (w < wv) woff += s_wsum[w];
+  const uint32_t excl = woff + incl - cnt;
+  const uint64_t toff = s_toff[0] + s_toff[1] + s_toff[2] + s_toff[3];
+  if (blockIdx.x + 1 == gridDim.x && tid == kStThreads - 1) {  // all matches
+    *A.total = toff + woff + incl;
+    if (A.total_host) *A.total_host = toff + woff + incl;  // pinned host memory, read after the batch's event
+  }
+  const uint32_t block_total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  if (ABL == 0) return;
+  const bool staged = block_total <= kEmStage;  // block-uniform
+  uint64_t o = toff + excl;
+  uint32_t so = excl;  // slot within the block
+#pragma unroll
+  for (int i = 0; i < kEmW; i++) {
+    uint64_t match = wm[i];
+    if (!match) continue;
+    const uint64_t p0 = (w0 + i) * 64;
+    uint32_t key = wk[i] & 0x7FFFFFFFu;
+    const bool cross = (wk[i] >> 31) != 0;  // a key starts inside this word
+    uint64_t kstart = 0, knext = 0;
+    if (cross) {
+      kstart = A.key_off[key];
+      knext = A.key_off[key + 1];
+    }
+    while (match) {
+      const int b = __builtin_ctzll(match);
+      match &= match - 1;
+      const uint64_t p = p0 + b;
+      uint32_t seq = ws[i] + (uint32_t)b;
+      if (cross) {
+        while (p >= knext) {  // the next key (empty keys share their offset: skipped too)
+          key++;
+          kstart = knext;
+          knext = A.key_off[key + 1];
+        }
+        seq = (uint32_t)(p - kstart);
+      }
+      if (staged) {
+        s_stage[so++] = uint2{key, seq};
+      } else if (o < A.out_cap) {
+        A.m_key[o] = key;
+#pragma unroll
+        for (int x = 0; x < M; x++) A.p_seq[o * M + x] = seq - x;
+      } else {
+        atomicOr(A.overflow, 1u);
+      }
+      o++;
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  if (ABL == 1) return;
+  // thread i writes matches i, i + 256, ...: adjacent threads, adjacent slots
+  for (uint32_t i = tid; i < block_total; i += kStThreads) {
+    const uint64_t slot = toff + i;
+    const uint2 e = s_stage[i];
+    if (slot < A.out_cap) {
+      A.m_key[slot] = e.x;
+      if (M == 3) {  // one 12-B store per match
+        *reinterpret_cast<uint3*>(A.p_seq + slot * 3) = uint3{e.y, e.y - 1, e.y - 2};
+      } else {
+#pragma unroll
+        for (int x = 0; x < M; x++) A.p_seq[slot * M + x] = e.y - x;
+      }
+    } else {
+      atomicOr(A.overflow, 1u);
+    }
+  }
+}
+
+
 template <class F>
 static float timeit(F f, int reps = 20) {
   hipEvent_t a, b;
@@ -200,6 +318,9 @@ int main(int argc, char** argv) {
   rep("stencil_emit", timeit([&] {
         hipLaunchKernelGGL(stencil_emit<3>, dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a);
       }));
+  rep("emit: loads + scans", timeit([&] { hipLaunchKernelGGL((emit_abl<3, 0>), dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a); }));
+  rep("emit: + LDS staging", timeit([&] { hipLaunchKernelGGL((emit_abl<3, 1>), dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a); }));
+  rep("emit: + writes", timeit([&] { hipLaunchKernelGGL((emit_abl<3, 2>), dim3((uint32_t)((n_tiles + kEmW - 1) / kEmW)), dim3(256), 0, 0, a); }));
   {
     uint64_t tt = 0;
     hipMemcpy(&tt, tot, 8, hipMemcpyDeviceToHost);

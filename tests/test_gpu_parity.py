@@ -176,6 +176,35 @@ def test_cfg3_medium_bit_exact():
     assert_parity(gpu_run(ir, off, cols), r, off)
 
 
+@pytest.mark.parametrize("query", ["readme", "cfg4s", "cfg4"])
+def test_full_size_digest_matches_oracle(query):
+    """ The benched configurations at their full size against the oracle,
+    not a key sample: config 3's 1e9 events over 1M keys (generated in HBM, the same bits as
+    workloads.generate) on the README query and on config 4's query, stress variant and as
+    written (NPE on about half of the keys) - match count, checksum over every (key, emission,
+    pairs) and the keys with an exception.  The README checksum is the bench line's
+    `a81bb860df5becf5`."""
+    cfg = W.CONFIGS[3]
+    stream = N.synth_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events)
+    q = W.stock_query("readme") if query == "readme" else W.any_kleene_query(carry_volume=(query == "cfg4s"))
+    ir = q.to_ir()
+    s = N.Session(N.Query(ir))
+    s.push_device(stream)
+    got = s.digest(0) + (int(np.count_nonzero(s.key_errors(0)[0])),)
+    s.close()
+    off, cols = stream.download()
+    del stream
+    r = oracle.run(ir, off, cols, threads=16)
+    emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+    pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+    pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+    want = (r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]),
+            int(np.count_nonzero(r["err_code"])))
+    assert got == want
+    if query == "readme":
+        assert f"{got[1]:016x}" == "a81bb860df5becf5"
+
+
 def test_cfg3_streaming_medium_bit_exact():
     """ The streaming path the processor runs, at scale against the oracle
     instead of the GPU's own per-batch checksum: config 3 at 20k keys (every 50th key of the
