@@ -60,7 +60,6 @@ struct Tuning {
   uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
   bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too
   bool no_spread = false;       // $CEP_NO_SPREAD: underfilled single-query launches not spread
-  uint32_t spread_waves = 0;    // $CEP_SPREAD_WAVES: waves a spread launch uses (0: the resident waves)
   uint32_t node_chunk = 0;      // $CEP_NODE_CHUNK: pool range per lane (0: default)
   uint32_t out_chunk = 0;       // $CEP_OUT_CHUNK
   uint32_t walk_cap = 0;        // $CEP_WALK_CAP: deferred walks per lane (0: default)

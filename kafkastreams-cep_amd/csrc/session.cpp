@@ -464,7 +464,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   uint64_t spread = 0;
   // (odd lanes take their row of ranks reversed: the slowest world-8 shard 16.5 -> 15.6 ms)
   if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64 && !s->tune.no_spread)
-    spread = std::min<uint64_t>(s->tune.spread_waves ? s->tune.spread_waves : resident / 64, nk);
+    spread = std::min<uint64_t>(resident / 64, nk);
   // (a full launch spread over all its waves - every wave led by one of the heaviest keys with
   // lighter ones beside it - was measured: cfg 3 29.2 -> 48.8 ms, every wave pays the divergence;
   // so was isolating a spread launch's heaviest ranks in waves of their own: the slowest world-8
