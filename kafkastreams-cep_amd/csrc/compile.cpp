@@ -698,6 +698,34 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   };
   loader("ld_ev", fields, ts);
   loader("ld_bev", bfields, bts);
+  // the begin predicate's columns for 4 consecutive positions p..p+3 (p % 4 == 0, all in the
+  // batch, columns 16-B aligned: bev4_aligned): 16-B loads (cep_nfa_bits)
+  o += "__device__ __forceinline__ bool bev4_aligned(const NfaArgs& A) {\n  return true";
+  for (uint32_t f = 0; f < d.n_fields; f++)
+    if (fields[f] && bfields[f] && d.field_type[f] != 0)
+      o += " && ((uint64_t)A.cols.p[" + std::to_string(f) + "] & 15u) == 0";
+  o += ";\n}\n";
+  o += "__device__ __forceinline__ void ld_bev4(Ev* e, const NfaArgs& A, uint64_t p) {\n";
+  for (uint32_t f = 0; f < d.n_fields; f++) {
+    if (!fields[f]) continue;
+    const std::string fs = "f" + std::to_string(f), col = "A.cols.p[" + std::to_string(f) + "]";
+    if (!bfields[f]) {
+      o += "  for (int j = 0; j < 4; j++) e[j]." + fs + " = 0;\n";
+    } else if (d.field_type[f] == 1) {
+      o += "  {\n    const int4 v = *reinterpret_cast<const int4*>((const int32_t*)" + col + " + p);\n";
+      o += "    e[0]." + fs + " = v.x;\n    e[1]." + fs + " = v.y;\n    e[2]." + fs + " = v.z;\n    e[3]." + fs + " = v.w;\n  }\n";
+    } else if (d.field_type[f] == 2 || d.field_type[f] == 3) {
+      const std::string ct = ctype(d.field_type[f]), vt = d.field_type[f] == 2 ? "longlong2" : "double2";
+      o += "  {\n    const " + vt + "* q = reinterpret_cast<const " + vt + "*>((const " + ct + "*)" + col + " + p);\n";
+      o += "    const " + vt + " a = q[0], b = q[1];\n";
+      o += "    e[0]." + fs + " = a.x;\n    e[1]." + fs + " = a.y;\n    e[2]." + fs + " = b.x;\n    e[3]." + fs + " = b.y;\n  }\n";
+    } else {
+      o += "  for (int j = 0; j < 4; j++) e[j]." + fs + " = ((const " + std::string(ctype(d.field_type[f])) + "*)" + col + ")[p + j];\n";
+    }
+  }
+  o += bts ? "  for (int j = 0; j < 4; j++) e[j].ts = A.ts ? A.ts[p + j] : (int64_t)(p + j);\n"
+           : "  for (int j = 0; j < 4; j++) e[j].ts = 0;\n";
+  o += "}\n";
   o += "\n";
   // predicates, one per (stage, edge); folds one per (stage, aggregate)
   std::string pa;
@@ -1001,11 +1029,13 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     // The begin predicate with null folds is true or throws at CSR position p, for any query
     // of the launch (a group kernel: the union over its queries' constants; each lane still
     // evaluates its own predicate there)
-    o += "__device__ __forceinline__ bool begin_hit_at(const NfaArgs& A, uint64_t p) {\n";
-    o += "  Ev e;\n  ld_bev(e, A, p);\n  const uint32_t nq = (NKC > 0 && A.n_q > 1) ? A.n_q : 1;\n";
+    o += "__device__ __forceinline__ bool begin_hit_ev(const NfaArgs& A, const Ev& e) {\n";
+    o += "  const uint32_t nq = (NKC > 0 && A.n_q > 1) ? A.n_q : 1;\n";
     o += "  for (uint32_t qi = 0; qi < nq; qi++) {\n    Kc K;\n    ld_kc(K, A, qi);\n    Fo f;\n";
     o += "    f.nm = (1u << F) - 1;\n    int err = 0;\n";
     o += "    if (" + predName[d.begin_stage][0] + "(e, f, err, K) || err) return true;\n  }\n  return false;\n}\n";
+    o += "__device__ __forceinline__ bool begin_hit_at(const NfaArgs& A, uint64_t p) {\n";
+    o += "  Ev e;\n  ld_bev(e, A, p);\n  return begin_hit_ev(A, e);\n}\n";
     // Work estimate per key for the lane order (session.cpp): the run-steps the key would take
     // if every run lived to the end, sum over begin hits b of (n - b), plus the quiet scan.
     // Read from the begin-hit bitmap (launched first): a lane per 64-event word, 1 bit per
@@ -1049,27 +1079,47 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
     o += "        m = y > m ? y : m;\n      }\n";
     o += "      if (threadIdx.x == 0) atomicMax(A.wmax, (unsigned long long)m ^ 0x8000000000000000ull);\n";
     o += "    }\n  }\n}\n\n";
-    // Begin-hit bitmap (NfaArgs.bhits): one thread per CSR position, a wave's ballot is one
-    // word.  Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).
-    // kBitStrips 256-position strips per block, their loads issued together (one position
-    // per thread per strip keeps every load instruction coalesced; few, longer workgroups:
-    // with 4 strips a 1e9-event batch was 1M workgroups of four loads each, 1.33 ms).
+    // Begin-hit bitmap (NfaArgs.bhits).  A block owns 256 * kBitStrips positions as strips of
+    // 1024: in a strip thread t holds positions 4t..4t+3 (16-B loads: 1 KiB a wave-instruction
+    // for a 4-byte column), and a wave's 256 positions make 4 bitmap words - word q from the
+    // ballots of lanes 16q..16q+15, bit 4i + j the j-th position of lane 16q + i (spread).
+    // Quiet lanes (only the begin run) jump from set bit to set bit (nfa_lane.h run).  (One
+    // position per thread and strip, 4-byte loads: 2.9 ms for 1e9 events with the watermark's
+    // timestamps, 4.1 TB/s.)
+    o += "__device__ __forceinline__ uint64_t bits_spread4(uint32_t x16) {\n  uint64_t x = x16;\n";
+    o += "  x = (x | (x << 24)) & 0x000000FF000000FFull;\n  x = (x | (x << 12)) & 0x000F000F000F000Full;\n";
+    o += "  x = (x | (x << 6)) & 0x0303030303030303ull;\n  x = (x | (x << 3)) & 0x1111111111111111ull;\n  return x;\n}\n";
     o += "extern \"C\" __global__ void __launch_bounds__(256) cep_nfa_bits(NfaArgs A) {\n";
-    o += "  constexpr int S = " + std::to_string(kBitStrips) + ";\n";
-    o += "  const uint64_t p0 = (uint64_t)blockIdx.x * (256 * S) + threadIdx.x;\n";
+    o += "  constexpr int S = " + std::to_string(kBitStrips / 4) + ";  // strips of 1024 positions\n";
+    o += "  const uint64_t b0 = (uint64_t)blockIdx.x * (256 * " + std::to_string(kBitStrips) + ");\n";
+    o += "  const uint64_t n = A.n_events;\n  const uint32_t lane = threadIdx.x & 63;\n";
     // the watermark's first level (session.cpp folds it here when the batch has timestamps): the
-    // block's largest event time.  Its S loads per thread are issued before the predicate's, and
-    // both before the bitmap stores (a store may alias them: loads after it waited for the
-    // predicate phase to finish - 2.9 ms for 1e9 events, 4.1 TB/s)
+    // block's largest event time; its loads issued before the predicate's, both before the
+    // bitmap stores (a store may alias them)
     o += "  const bool wmf = A.wm_blocks != nullptr;\n";
-    o += "  int64_t t[S];\n#pragma unroll\n  for (int k = 0; k < S; k++) {\n";
-    o += "    const uint64_t p = p0 + (uint64_t)k * 256;\n    t[k] = wmf && p < A.n_events ? A.ts[p] : INT64_MIN;\n  }\n";
-    o += "  bool h[S];\n#pragma unroll\n  for (int k = 0; k < S; k++) {\n";
-    o += "    const uint64_t p = p0 + (uint64_t)k * 256;\n    h[k] = p < A.n_events && begin_hit_at(A, p);\n  }\n";
-    o += "  int64_t m = t[0];\n#pragma unroll\n  for (int k = 1; k < S; k++) m = t[k] > m ? t[k] : m;\n";
-    o += "#pragma unroll\n  for (int k = 0; k < S; k++) {\n    const uint64_t p = p0 + (uint64_t)k * 256;\n";
-    o += "    const uint64_t b = __ballot(h[k]);\n";
-    o += "    if ((threadIdx.x & 63) == 0 && p < A.n_events) A.bhits[p >> 6] = b;\n  }\n";
+    o += "  const bool vec = bev4_aligned(A) && (!wmf || ((uint64_t)A.ts & 15u) == 0);\n";
+    o += "  int64_t t[S][4];\n#pragma unroll\n  for (int k = 0; k < S; k++) {\n";
+    o += "    const uint64_t p = b0 + (uint64_t)k * 1024 + (uint64_t)threadIdx.x * 4;\n";
+    o += "    if (wmf && vec && p + 4 <= n) {\n";
+    o += "      const longlong2* q = reinterpret_cast<const longlong2*>(A.ts + p);\n";
+    o += "      const longlong2 a = q[0], c = q[1];\n";
+    o += "      t[k][0] = a.x;\n      t[k][1] = a.y;\n      t[k][2] = c.x;\n      t[k][3] = c.y;\n";
+    o += "    } else {\n#pragma unroll\n      for (int j = 0; j < 4; j++) t[k][j] = wmf && p + j < n ? A.ts[p + j] : INT64_MIN;\n    }\n  }\n";
+    o += "  bool h[S][4];\n#pragma unroll\n  for (int k = 0; k < S; k++) {\n";
+    o += "    const uint64_t p = b0 + (uint64_t)k * 1024 + (uint64_t)threadIdx.x * 4;\n    Ev e[4];\n";
+    o += "    if (vec && p + 4 <= n) {\n      ld_bev4(e, A, p);\n    } else {\n";
+    o += "#pragma unroll\n      for (int j = 0; j < 4; j++) ld_bev(e[j], A, p + j < n ? p + j : 0);\n    }\n";
+    o += "#pragma unroll\n    for (int j = 0; j < 4; j++) h[k][j] = p + j < n && begin_hit_ev(A, e[j]);\n  }\n";
+    o += "  int64_t m = INT64_MIN;\n#pragma unroll\n  for (int k = 0; k < S; k++)\n#pragma unroll\n";
+    o += "    for (int j = 0; j < 4; j++) m = t[k][j] > m ? t[k][j] : m;\n";
+    o += "#pragma unroll\n  for (int k = 0; k < S; k++) {\n    uint64_t B[4];\n";
+    o += "#pragma unroll\n    for (int j = 0; j < 4; j++) B[j] = __ballot(h[k][j]);\n";
+    o += "    uint64_t w = 0;  // lane q < 4: word q of the wave's 256 positions\n";
+    o += "#pragma unroll\n    for (int q = 0; q < 4; q++) {\n      uint64_t x = 0;\n";
+    o += "#pragma unroll\n      for (int j = 0; j < 4; j++) x |= bits_spread4((uint32_t)(B[j] >> (16 * q)) & 0xFFFFu) << j;\n";
+    o += "      if (lane == (uint32_t)q) w = x;\n    }\n";
+    o += "    const uint64_t ws = b0 + (uint64_t)k * 1024 + (uint64_t)(threadIdx.x >> 6) * 256 + (uint64_t)lane * 64;\n";
+    o += "    if (lane < 4 && ws < n) A.bhits[ws >> 6] = w;\n  }\n";
     o += "  if (wmf) {\n";
     o += "    for (int o = 32; o > 0; o >>= 1) {\n      const int64_t y = __shfl_down(m, o, 64);\n      m = y > m ? y : m;\n    }\n";
     o += "    __shared__ int64_t wm[4];\n    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;\n    __syncthreads();\n";

@@ -25,6 +25,17 @@
 #define CEP_LDS_AS           // (no address spaces on the host)
 #define asm(...) ((void)0)
 
+// (the vector types the generated bitmap kernel's 16-B loads use)
+struct int4 {
+  int x, y, z, w;
+};
+struct longlong2 {
+  long long x, y;
+};
+struct double2 {
+  double x, y;
+};
+
 struct LaneDim3 {
   unsigned x = 0, y = 0, z = 0;
 };
