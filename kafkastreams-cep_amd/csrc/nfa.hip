@@ -336,7 +336,10 @@ struct HeavyKey {
   uint32_t key, pad;
   uint64_t mo, po;  // its first match / pair index in the flat arrays
 };
-constexpr uint32_t kHeavyPairs = 2048;
+// (a key from 64 pairs on: config 3's matching keys hold ~25-50; the per-thread walk of them
+// scattered its writes across lanes - 0.87 ms against 0.23 + 0.26 ms this way, cfg 3; from
+// 16 pairs on and twice the waves 0.19 + 0.38)
+constexpr uint32_t kHeavyPairs = 64;
 
 __global__ void __launch_bounds__(256) scatter_matches(const KeyState* ks, uint64_t n, const uint64_t* bsum_m,
                                                        const uint64_t* bsum_p, const uint32_t* out,
@@ -585,7 +588,7 @@ hipError_t launch_scatter(const KeyState* ks, uint64_t n_keys, const uint64_t* b
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(scatter_matches, dim3((uint32_t)nb), dim3(256), 0, st, ks, n_keys, bsum_m, bsum_p, out,
                      m_key, m_emit, m_off, p_seq, p_stage, totals, heavy, n_heavy);
-  hipLaunchKernelGGL(scatter_heavy, dim3(1024), dim3(256), 0, st, ks, heavy, n_heavy, out, m_key, m_emit, m_off,
+  hipLaunchKernelGGL(scatter_heavy, dim3(4096), dim3(256), 0, st, ks, heavy, n_heavy, out, m_key, m_emit, m_off,
                      p_seq, p_stage);
   return hipGetLastError();
 }
