@@ -15,7 +15,8 @@ import cepamd  # noqa: E402,F401
 from kafkastreams_cep_amd import native as N  # noqa: E402
 from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
-KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST")
+KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST",
+         "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS")
 DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
 
 
