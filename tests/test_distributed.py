@@ -101,6 +101,52 @@ def test_kafka_partitioner_is_a_partition():
         assert int(SH.murmur2_int_keys([key])[0]) == murmur2_scalar(key)
 
 
+def _murmur2_bytes(data: bytes) -> int:
+    """Kafka's Utils.murmur2 over any byte array (clients/.../common/utils/Utils.java), as a
+    signed Java int: 4-byte little-endian blocks, then the 1-3 tail bytes, then the final mix."""
+    m = 0x5BD1E995
+    h = (0x9747B28C ^ len(data)) & 0xFFFFFFFF
+    for i in range(len(data) // 4):
+        k = data[4 * i] | data[4 * i + 1] << 8 | data[4 * i + 2] << 16 | data[4 * i + 3] << 24
+        k = (k * m) & 0xFFFFFFFF
+        k ^= k >> 24
+        k = (k * m) & 0xFFFFFFFF
+        h = ((h * m) & 0xFFFFFFFF) ^ k
+    rem, b = len(data) % 4, len(data) & ~3
+    if rem == 3:
+        h ^= data[b + 2] << 16
+    if rem >= 2:
+        h ^= data[b + 1] << 8
+    if rem >= 1:
+        h = ((h ^ data[b]) * m) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * m) & 0xFFFFFFFF
+    h ^= h >> 15
+    return h - (1 << 32) if h >= 1 << 31 else h
+
+
+def test_murmur2_pinned_by_kafka_vectors():
+    """(murmur2 was parity unpinned) The partitioner's hash against the test
+    vectors Kafka publishes for Utils.murmur2 (kafka-clients UtilsTest.testMurmur2; Kafka is a
+    dependency of the reference, not part of /root/reference): the general byte-array form
+    reproduces all six, and the partitioner's 4-byte key path (shard.murmur2_int_keys, the
+    big-endian serialization of each u32 key id) equals it on every key of a sample."""
+    sys.path[:0] = [ROOT]
+    import cepamd  # noqa: F401
+    from kafkastreams_cep_amd import shard as SH
+
+    kafka = {b"21": -973932308, b"foobar": -790332482, b"a-little-bit-long-string": -985981536,
+             b"a-little-bit-longer-string": -1486304829,
+             b"lkjh234lh9fiuh90y23oiuhsafujhadof229phr9h19h89h8": -58897971, b"abc": 479470107}
+    for data, want in kafka.items():
+        assert _murmur2_bytes(data) == want, data
+    keys = np.concatenate([np.arange(5000, dtype=np.uint32),
+                           np.random.default_rng(5).integers(0, 2**32, 5000, dtype=np.uint64).astype(np.uint32)])
+    got = SH.murmur2_int_keys(keys).astype(np.int64)
+    want = np.array([_murmur2_bytes(int(k).to_bytes(4, "big")) & 0xFFFFFFFF for k in keys], np.int64)
+    np.testing.assert_array_equal(got, want)
+
+
 def test_two_rank_sharding_matches_single_rank():
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     with tempfile.TemporaryDirectory() as d:
