@@ -60,6 +60,7 @@ struct Tuning {
   uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
   bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too
   bool no_spread = false;       // $CEP_NO_SPREAD: underfilled single-query launches not spread
+  bool no_retry = false;        // $CEP_NO_RETRY: capacity / conflict re-runs skipped (their keys keep the error)
   uint32_t node_chunk = 0;      // $CEP_NODE_CHUNK: pool range per lane (0: default)
   uint32_t out_chunk = 0;       // $CEP_OUT_CHUNK
   uint32_t walk_cap = 0;        // $CEP_WALK_CAP: deferred walks per lane (0: default)

@@ -751,6 +751,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   g.stats.main_ms = main_ms;
   g.stats.retried_jobs = widened;  // (streams: the keys the wide build continued)
   g.stats.retry_ms = widen_ms;
+  if (s->tune.no_retry) h.n_cap_err = 0;  // (measurement runs: which keys a build cannot finish)
   for (int round = 0; h.n_cap_err > 0 && round < 8; round++) {
     const uint64_t nlist = h.n_cap_err;
     s->keylist.ensure(sizeof(uint32_t) * 2 * nlist);

@@ -30,6 +30,7 @@ Tuning tuning_from_env() {
   t.resident_waves = rw > 0 ? (uint32_t)rw : 0u;
   t.no_persist = flag("CEP_NO_PERSIST");
   t.no_spread = flag("CEP_NO_SPREAD");
+  t.no_retry = flag("CEP_NO_RETRY");
   const long nc = num("CEP_NODE_CHUNK", 0), oc = num("CEP_OUT_CHUNK", 0), wc = num("CEP_WALK_CAP", 0);
   t.node_chunk = nc > 0 ? (uint32_t)nc : 0u;
   t.out_chunk = oc > 0 ? (uint32_t)oc : 0u;
