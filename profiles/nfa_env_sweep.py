@@ -36,7 +36,8 @@ def query(name, env, variant):
     if variant.startswith("mq"):  # one of config 5's variants, e.g. mq63
         ir = W.multi_queries(64)[int(variant[2:])].to_ir()
     else:
-        ir = W.stock_query(variant).to_ir() if variant != "any" else W.any_kleene_query().to_ir()
+        ir = (W.any_kleene_query().to_ir() if variant == "any" else
+              W.any_kleene_query(carry_volume=True).to_ir() if variant == "anys" else W.stock_query(variant).to_ir())
     q = N.Query(ir)
     for k in KNOBS:
         os.environ.pop(k, None)
