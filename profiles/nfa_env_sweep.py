@@ -16,7 +16,7 @@ from kafkastreams_cep_amd import native as N  # noqa: E402
 from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
 KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST",
-         "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS")
+         "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS", "CEP_STREAM_PAIRS")
 DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
 
 
@@ -40,7 +40,8 @@ def query(name, env, variant):
               W.any_kleene_query(carry_volume=True).to_ir() if variant == "anys" else W.stock_query(variant).to_ir())
     q = N.Query(ir)
     for k in KNOBS:
-        os.environ.pop(k, None)
+        if k != "CEP_STREAM_PAIRS":  # (read again when a streaming session builds its kernel)
+            os.environ.pop(k, None)
     return q
 
 
@@ -51,11 +52,14 @@ def main():
     ap.add_argument("--query", default="readme")
     ap.add_argument("--variants", default=DEFAULT)
     ap.add_argument("--precompile", action="store_true")
+    ap.add_argument("--stream", action="store_true",
+                    help="one push of the whole batch into a fresh streaming session per step (stream build)")
     args = ap.parse_args()
     vs = parse(args.variants)
     if args.precompile:
         for name, env in vs:
             print(name, query(name, env, args.query).precompile())
+            os.environ.pop("CEP_STREAM_PAIRS", None)
         return
     cfg = W.CONFIGS[3]
     stream = N.synth_stream("stock", cfg.seed, args.keys, cfg.mean_events)
@@ -64,15 +68,25 @@ def main():
         qq = query(name, env, args.query)
         if "CEP_NO_PERSIST" in env:  # read by the session at each batch
             os.environ["CEP_NO_PERSIST"] = env["CEP_NO_PERSIST"]
-        s = N.Session(qq)
-        s.push_device(stream)
         ks = []
-        for _ in range(args.steps):
+        if args.stream:  # a stream carries its keys' runs: a fresh session per step
+            for _ in range(args.steps + 1):
+                s = N.Session(qq, streaming=True)
+                s.push_device(stream)
+                ks.append(s.timing(0)[0])
+                if _ < args.steps:
+                    s.close()
+            ks = ks[1:]
+        else:
+            s = N.Session(qq)
             s.push_device(stream)
-            ks.append(s.timing(0)[0])
+            for _ in range(args.steps):
+                s.push_device(stream)
+                ks.append(s.timing(0)[0])
         n, d = s.digest(0)
         code, _ = s.key_errors(0)
         os.environ.pop("CEP_NO_PERSIST", None)
+        os.environ.pop("CEP_STREAM_PAIRS", None)
         res[name] = {"kernel_ms": min(ks), "all_ms": ks, "matches": n, "checksum": f"{d:016x}",
                      "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2], "stats": s.stats(0)}
         print(name, json.dumps(res[name]), flush=True)
