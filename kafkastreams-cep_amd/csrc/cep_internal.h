@@ -3,7 +3,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -126,15 +125,15 @@ inline std::string jit_wide_source(const std::string& src) { return "#define CEP
 // launch); the put log (a stream cannot re-run a key: walk conflicts resolved in place); a key
 // whose versions outgrow 3 pairs stops before that event for the wide build to continue
 // (CEP_STREAM_STOP, nfa_lane.h stop_event)
-// ($CEP_STREAM_PAIRS: the stream build's register pairs, measurement builds only)
+// the stream build's register pairs, memory-layout pairs and put log: 3, 6, 1 (measurement
+// builds, tuning.cpp: $CEP_STREAM_PAIRS, $CEP_STREAM_LAYOUT, $CEP_STREAM_PUTLOG=0 - the last
+// two inexact for streams, for timing what they cost)
+void tuning_stream_build(int* pairs, int* layout, int* plog);
 inline std::string jit_stream_source(const std::string& src) {
-  int pairs = 3;
-#ifdef CEP_MEASURE
-  if (const char* v = std::getenv("CEP_STREAM_PAIRS"))
-    if (std::atoi(v) > 0 && std::atoi(v) < 6) pairs = std::atoi(v);
-#endif
-  return "#define CEP_DEWEY_PAIRS " + std::to_string(pairs) +
-         "\n#define CEP_LAYOUT_PAIRS 6\n#define CEP_PUT_LOG 1\n#define CEP_STREAM_STOP 1\n"
+  int pairs = 3, layout = 6, plog = 1;
+  tuning_stream_build(&pairs, &layout, &plog);
+  return "#define CEP_DEWEY_PAIRS " + std::to_string(pairs) + "\n#define CEP_LAYOUT_PAIRS " + std::to_string(layout) +
+         "\n#define CEP_PUT_LOG " + std::to_string(plog) + "\n#define CEP_STREAM_STOP 1\n"
          "#define CEP_PERSIST_LANES 0\n#define CEP_WAVES_EU 3\n" + src;
 }
 struct Cols;

@@ -24,6 +24,13 @@ uint32_t tuning_walk_flush() {
   return v > 0 ? (uint32_t)v : 24u;
 }
 
+void tuning_stream_build(int* pairs, int* layout, int* plog) {
+  const long p = num("CEP_STREAM_PAIRS", 3), l = num("CEP_STREAM_LAYOUT", 6);
+  *pairs = p > 0 && p < 6 ? (int)p : 3;
+  *layout = l >= *pairs && l <= 6 ? (int)l : 6;
+  *plog = num("CEP_STREAM_PUTLOG", 1) ? 1 : 0;
+}
+
 Tuning tuning_from_env() {
   Tuning t;
   const long rw = num("CEP_RESIDENT_WAVES", 0);
@@ -57,6 +64,7 @@ Tuning tuning_from_env() {
 }
 #else
 uint32_t tuning_walk_flush() { return 24u; }
+void tuning_stream_build(int*, int*, int*) {}
 Tuning tuning_from_env() { return Tuning{}; }
 #endif
 

@@ -16,7 +16,8 @@ from kafkastreams_cep_amd import native as N  # noqa: E402
 from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
 KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST",
-         "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS", "CEP_STREAM_PAIRS")
+         "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS", "CEP_STREAM_PAIRS",
+         "CEP_STREAM_LAYOUT", "CEP_STREAM_PUTLOG")
 DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
 
 
@@ -40,7 +41,7 @@ def query(name, env, variant):
               W.any_kleene_query(carry_volume=True).to_ir() if variant == "anys" else W.stock_query(variant).to_ir())
     q = N.Query(ir)
     for k in KNOBS:
-        if k != "CEP_STREAM_PAIRS":  # (read again when a streaming session builds its kernel)
+        if not k.startswith("CEP_STREAM_"):  # (read again when a streaming session builds its kernel)
             os.environ.pop(k, None)
     return q
 
@@ -59,7 +60,8 @@ def main():
     if args.precompile:
         for name, env in vs:
             print(name, query(name, env, args.query).precompile())
-            os.environ.pop("CEP_STREAM_PAIRS", None)
+            for k in KNOBS:
+                os.environ.pop(k, None)
         return
     cfg = W.CONFIGS[3]
     stream = N.synth_stream("stock", cfg.seed, args.keys, cfg.mean_events)
@@ -86,7 +88,8 @@ def main():
         n, d = s.digest(0)
         code, _ = s.key_errors(0)
         os.environ.pop("CEP_NO_PERSIST", None)
-        os.environ.pop("CEP_STREAM_PAIRS", None)
+        for k in KNOBS:
+            os.environ.pop(k, None)
         res[name] = {"kernel_ms": min(ks), "all_ms": ks, "matches": n, "checksum": f"{d:016x}",
                      "key_errors": int((code != 0).sum()), "launches": s.timing(0)[2], "stats": s.stats(0)}
         print(name, json.dumps(res[name]), flush=True)
