@@ -14,6 +14,7 @@ namespace cep {
 
 // 256-position strips per workgroup of the begin-hit bitmap kernel (compile.cpp cep_nfa_bits)
 constexpr int kBitStrips = 16;
+static_assert(kBitStrips % 4 == 0, "cep_nfa_bits covers a block's positions as kBitStrips / 4 strips of 1024");
 struct ParsedQuery;
 }
 
@@ -54,8 +55,8 @@ std::vector<GroupPlan> plan_groups(const std::vector<const cep_query*>& qs);
 // Measurement knobs ($CEP_* environment variables).  Read only by the measurement
 // build (libcep_measure.so: CEP_MEASURE, Makefile `measure`), once, when a session is created
 // (tuning.cpp) - never on the launch path - and kept in the session; the release build uses the
-// defaults below.  Results never depend on them; only the launch geometry and the time a batch
-// takes do.
+// defaults below.  Most change only the launch geometry and the time a batch takes; the few that
+// change results (timing and diagnosis only) are listed in tuning.cpp's header.
 struct Tuning {
   uint32_t resident_waves = 0;  // $CEP_RESIDENT_WAVES: waves per CU of the persistent grids (0: default)
   bool no_persist = false;      // $CEP_NO_PERSIST: one lane per job for kernel groups too

@@ -540,6 +540,7 @@ void usesM(const M* m, std::vector<bool>& fields, bool& ts) {
 // that read it and the exec-mask work around them.  Returns per stage the may-be-null mask of
 // its dispatch case (-1: no queued record reaches it), or an empty vector when the search
 // outgrew its budget (no masking).
+static_assert(kMaxStates <= 32, "fold_nullness keeps a fold slot's null bit as 1u << slot");
 static std::vector<int64_t> fold_nullness(const cep_query* q, const Builder& b) {
   const DevQuery& d = q->dev;
   const uint32_t all = d.n_states >= 32 ? ~0u : (1u << d.n_states) - 1u;

@@ -52,12 +52,20 @@ static thread_local uint32_t g_allocs = 0;
 // $CEP_POISON=mask (measurement runs): the session's k-th device allocation (k < 64, bit k of
 // the mask; -1: all) filled with 0xFF bytes (CEP_NONE words; $CEP_POISON_BYTE another byte), so a read of memory no kernel wrote is not hidden
 // by a fresh allocation's zeros
-static uint64_t g_poison = 0;
-static uint32_t g_poison_base = 0;
-static int g_poison_byte = 0xFF;  // ($CEP_POISON_BYTE)
+// (thread_local like g_allocs: one session per thread, each thread's allocation index against its
+// own base)
+static thread_local uint64_t g_poison = 0;
+static thread_local uint32_t g_poison_base = 0;
+static thread_local int g_poison_byte = 0xFF;  // ($CEP_POISON_BYTE)
 static bool poison_next() {
   const uint32_t k = g_allocs - g_poison_base;
   return k < 64 && ((g_poison >> k) & 1u);
+}
+// A copy on the session's own stream, waited for.  Session paths never use the null stream:
+// it does not order with the sessions' hipStreamNonBlocking streams.
+static void copy_sync(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t st) {
+  HIPCHECK(hipMemcpyAsync(dst, src, n, k, st));
+  HIPCHECK(hipStreamSynchronize(st));
 }
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -460,7 +468,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   // multi-GPU run, a small batch) is as long as its longest wave, whose length is its heaviest
   // key's chain of events times the wave's per-event cost; that cost grows with the number of
   // divergent lanes.  So its keys are spread over every wave slot the chip holds: the heaviest
-  // keys lead one wave each, with lighter keys beside them ($CEP_SPREAD=0: measurement runs).
+  // keys lead one wave each, with lighter keys beside them ($CEP_NO_SPREAD: measurement runs).
   uint64_t spread = 0;
   // (odd lanes take their row of ranks reversed: the slowest world-8 shard 16.5 -> 15.6 ms)
   if (!persist && Q == 1 && nk > 64 && (nk + 63) / 64 < resident / 64 && !s->tune.no_spread)
@@ -677,7 +685,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   if (wm_here) s->watermark = (int64_t)(h.wmax ^ 0x8000000000000000ull);
   if (prof) {  // one line per launch on stderr: the counters of nfa_lane.h's CEP_PROF list
     unsigned long long pc[16];
-    HIPCHECK(hipMemcpy(pc, s->prof.p, sizeof pc, hipMemcpyDeviceToHost));
+    copy_sync(pc, s->prof.p, sizeof pc, hipMemcpyDeviceToHost, s->stream);
     std::fprintf(stderr, "cep_prof {\"jobs\": %llu, \"c\": [", (unsigned long long)jobs);
     for (int i = 0; i < 14; i++) std::fprintf(stderr, "%s%llu", i ? ", " : "", pc[i]);
     std::fprintf(stderr, "]}\n");
@@ -724,7 +732,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
   }
   if (streaming) {  // no re-runs: a key that hit a limit keeps its error (sticky, reported)
     uint32_t tops[2];
-    HIPCHECK(hipMemcpy(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost));
+    copy_sync(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost, s->stream);
     S.node_used = (uint32_t)std::min<uint64_t>(tops[0], S.node_cap);
     S.pred_used = (uint32_t)std::min<uint64_t>(tops[1], S.pred_cap);
     h.n_cap_err = 0;
@@ -1023,10 +1031,10 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
       r->q = queries[i];
       r->F = queries[i]->F;  // fold slots of a run record (compile.cpp)
       r->d_q.ensure(sizeof(DevQuery));
-      HIPCHECK(hipMemcpy(r->d_q.p, &queries[i]->dev, sizeof(DevQuery), hipMemcpyHostToDevice));
+      copy_sync(r->d_q.p, &queries[i]->dev, sizeof(DevQuery), hipMemcpyHostToDevice, s->stream);
       r->d_code.ensure(sizeof(uint32_t) * queries[i]->code.size());
-      HIPCHECK(hipMemcpy(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
-                         hipMemcpyHostToDevice));
+      copy_sync(r->d_code.p, queries[i]->code.data(), sizeof(uint32_t) * queries[i]->code.size(),
+                hipMemcpyHostToDevice, s->stream);
       s->qs.push_back(std::move(r));
     }
     // kernel groups: the JIT tier of a per-batch session runs queries that differ only in
@@ -1098,7 +1106,7 @@ int cep_session_create(const cep_query* const* queries, int n_queries, const cep
       }
       if (pl.nkc) {
         g->kc.ensure(sizeof(int64_t) * pl.table.size());
-        HIPCHECK(hipMemcpy(g->kc.p, pl.table.data(), sizeof(int64_t) * pl.table.size(), hipMemcpyHostToDevice));
+        copy_sync(g->kc.p, pl.table.data(), sizeof(int64_t) * pl.table.size(), hipMemcpyHostToDevice, s->stream);
       }
       s->groups.push_back(std::move(g));
     }
@@ -1496,7 +1504,7 @@ int cep_session_snapshot(cep_session* s, void* buf, size_t cap, size_t* size) {
       o += sizeof h;
       if (!S.init) continue;
       auto d2h = [&](const void* src, uint64_t n) {
-        if (n) HIPCHECK(hipMemcpy(o, src, n, hipMemcpyDeviceToHost));
+        if (n) copy_sync(o, src, n, hipMemcpyDeviceToHost, s->stream);
         o += n;
       };
       d2h(S.carry.p, sizeof(KeyCarry) * std::max<uint64_t>(S.n_keys, 1));
@@ -1576,7 +1584,7 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size) {
       if (!h.init) continue;
       auto h2d = [&](DBuf& dst, uint64_t n) {
         dst.ensure(std::max<uint64_t>(n, 16));
-        if (n) HIPCHECK(hipMemcpy(dst.p, q, n, hipMemcpyHostToDevice));
+        if (n) copy_sync(dst.p, q, n, hipMemcpyHostToDevice, s->stream);
         q += n;
       };
       S.n_keys = h.n_keys;
@@ -1593,7 +1601,7 @@ int cep_session_restore(cep_session* s, const void* buf, size_t size) {
       S.pred_used = h.pred_used;
       const uint32_t tops[2] = {h.node_used, h.pred_used};
       S.tops.ensure(2 * sizeof(uint32_t));
-      HIPCHECK(hipMemcpy(S.tops.p, tops, sizeof tops, hipMemcpyHostToDevice));
+      copy_sync(S.tops.p, tops, sizeof tops, hipMemcpyHostToDevice, s->stream);
       S.init = true;
     }
     s->watermark = wm;
@@ -1726,7 +1734,13 @@ int cep_memcpy(void* dst, const void* src, size_t bytes, int dst_memory, int src
                                                                                   : hipMemcpyHostToDevice)
                                                  : (src_memory == CEP_MEM_DEVICE ? hipMemcpyDeviceToHost
                                                                                   : hipMemcpyHostToHost);
-  return guarded([&] { HIPCHECK(hipMemcpy(dst, src, bytes, k)); });
+  // (a caller's copy of a session's device results: every stream's work on them done first - the
+  // stencil path returns without a host sync, and the null stream does not order with the
+  // sessions' non-blocking streams)
+  return guarded([&] {
+    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipMemcpy(dst, src, bytes, k));
+  });
 }
 
 int cep_decode_stock_json(int device, const uint8_t* bytes, const uint64_t* rec_off, uint64_t n_records,

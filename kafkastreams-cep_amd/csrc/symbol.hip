@@ -278,15 +278,23 @@ hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint
   uint64_t cap = 1024;
   const uint64_t want = 2 * (max_symbols < n ? max_symbols : n);
   while (cap < want) cap <<= 1;
-  unsigned long long* tab_hash = nullptr;
-  uint32_t *tab_rep = nullptr, *slot_of = nullptr, *first = nullptr, *prefix = nullptr, *err = nullptr, *stmp = nullptr;
-  hipError_t e = hipSuccess;
+  // One plain device allocation carved into the call's arrays (no stream-ordered pool: every
+  // device allocation of the library is hipMalloc, freed after the call's stream is drained;
+  // DESIGN.md §7 "the arrival-order flake").  Layout: hash table (8 B), then u32 arrays.
+  const uint64_t w_rep = cap, w_slot = n, w_first = n, w_prefix = n + 1, w_err = 1, w_stmp = scan_u32_scratch(n) + 1;
+  const size_t block_bytes = 8 * cap + 4 * (w_rep + w_slot + w_first + w_prefix + w_err + w_stmp);
+  void* block = nullptr;
+  hipError_t e = hipMalloc(&block, block_bytes);
+  if (e != hipSuccess) return e;
+  unsigned long long* tab_hash = (unsigned long long*)block;
+  uint32_t* tab_rep = (uint32_t*)(tab_hash + cap);
+  uint32_t* slot_of = tab_rep + w_rep;
+  uint32_t* first = slot_of + w_slot;
+  uint32_t* prefix = first + w_first;
+  uint32_t* err = prefix + w_prefix;
+  uint32_t* stmp = err + w_err;
   auto ok = [&](hipError_t x) { if (e == hipSuccess) e = x; return e == hipSuccess; };
-  if (ok(hipMallocAsync((void**)&tab_hash, 8 * cap, st)) && ok(hipMallocAsync((void**)&tab_rep, 4 * cap, st)) &&
-      ok(hipMallocAsync((void**)&slot_of, 4 * n, st)) && ok(hipMallocAsync((void**)&first, 4 * n, st)) &&
-      ok(hipMallocAsync((void**)&prefix, 4 * (n + 1), st)) && ok(hipMallocAsync((void**)&err, 4, st)) &&
-      ok(hipMallocAsync((void**)&stmp, 4 * (scan_u32_scratch(n) + 1), st)) &&
-      ok(hipMemsetAsync(tab_hash, 0, 8 * cap, st)) && ok(hipMemsetAsync(tab_rep, 0xFF, 4 * cap, st)) &&
+  if (ok(hipMemsetAsync(tab_hash, 0, 8 * cap, st)) && ok(hipMemsetAsync(tab_rep, 0xFF, 4 * cap, st)) &&
       ok(hipMemsetAsync(err, 0, 4, st))) {
     const dim3 g((uint32_t)((n + 255) / 256));
     hipLaunchKernelGGL(sym_insert, g, dim3(256), 0, st, bytes, rec_off, span, status, n, tab_hash, tab_rep, cap - 1,
@@ -301,9 +309,9 @@ hipError_t symbol_keys(const uint8_t* bytes, const uint64_t* rec_off, const uint
         *n_symbols = (uint64_t)last[0] + last[1];
     }
   }
-  for (void* p : {(void*)tab_hash, (void*)tab_rep, (void*)slot_of, (void*)first, (void*)prefix, (void*)err, (void*)stmp})
-    if (p) (void)hipFreeAsync(p, st);
+  // the call's kernels are done before the block goes back (hipFree also waits for the device)
   (void)hipStreamSynchronize(st);
+  (void)hipFree(block);
   return e;
 }
 

@@ -3,7 +3,10 @@
 // knobs compiled into a query's kernel, at query compile.  Only the measurement build reads
 // the environment (CEP_MEASURE: libcep_measure.so, Makefile `measure`); the release libcep.so
 // runs the defaults and calls getenv for $CEP_JIT_CACHE alone (tests/test_native_abi.py).
-// Results never depend on these knobs.
+// Most knobs change only launch geometry and timing; these change results and are for timing
+// and diagnosis only: $CEP_NO_RETRY (keys keep their capacity / conflict error), $CEP_STREAM_PUTLOG=0
+// and $CEP_STREAM_LAYOUT < 6 (inexact for streams), $CEP_POISON (buffer contents before first
+// write), $CEP_DEWEY_PAIRS (fewer pairs: more keys re-run or fail).
 #include <cstdlib>
 
 #include "cep_internal.h"

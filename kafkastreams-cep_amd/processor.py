@@ -98,7 +98,10 @@ _EXC = {1: NullPointerException, 2: IllegalStateException, 3: ArithmeticExceptio
 
 NFA_STATES_STORE = "_cep_nfa"  # CEPProcessor.java:56
 _CKPT_MAGIC = b"CEPPROC2"  # 2: plain encoding (JSON host half); 1 (pickle) is not read
-_CKPT_VERSION = 2
+# host-half versions: 3 = JsonSerde's tagged encoding (tuples, bytes, numpy scalars, non-string
+# dict keys); 2 = the plain JSON encoding before it (read back with plain json.loads)
+_CKPT_VERSION = 3
+_CKPT_READABLE = (2, 3)
 
 
 class JsonSerde:
@@ -163,6 +166,11 @@ class JsonSerde:
     @classmethod
     def deserialize(cls, data: bytes):
         return cls._dec(json.loads(data.decode()))
+
+    @classmethod
+    def deserialize_v2(cls, data: bytes):
+        """A value a version-2 checkpoint holds: plain JSON (a dict with a "__cep__" key is data)."""
+        return json.loads(data.decode())
 
 
 # ---- Event / Sequence ---------------------------------------------------------------------
@@ -383,12 +391,18 @@ class CEPProcessor:
             raise ValueError("not a CEPProcessor checkpoint (or an older, unsupported version)")
         n = int.from_bytes(blob[8:16], "little")
         host = json.loads(blob[16 + n:].decode())
-        if not isinstance(host, dict) or host.get("version") != _CKPT_VERSION:
+        if not isinstance(host, dict) or host.get("version") not in _CKPT_READABLE:
             raise ValueError("unsupported CEPProcessor checkpoint version")
         if host["ir"] != self.ir.hex() or host["max_keys"] != self.max_keys:
             raise ValueError("checkpoint of another pattern or key space")
-        keys = [self.key_serde.deserialize(base64.b64decode(k)) for k in host["keys"]]
-        events = [[Event(k, self.value_serde.deserialize(base64.b64decode(v)), ts, topic, part, off)
+
+        def dec(serde):  # (version 2: the default serde wrote plain JSON)
+            if host["version"] == 2 and ((isinstance(serde, type) and issubclass(serde, JsonSerde)) or isinstance(serde, JsonSerde)):
+                return serde.deserialize_v2
+            return serde.deserialize
+        kdec, vdec = dec(self.key_serde), dec(self.value_serde)
+        keys = [kdec(base64.b64decode(k)) for k in host["keys"]]
+        events = [[Event(k, vdec(base64.b64decode(v)), ts, topic, part, off)
                    for ts, topic, part, off, v in evs] for k, evs in zip(keys, host["events"])]
         if not (len(events) == len(keys) == len(host["base"]) == len(host["total"])):
             raise ValueError("malformed CEPProcessor checkpoint")

@@ -2,7 +2,7 @@
 # Round 5: wave-cooperative walk hops on config 5 (nfa_lane.h coop_hops).  The cfg 5 GPU
 # parity tests, then batches 0 and 3 of the 64-variant group at the default threshold (8
 # walkers) and, in the measurement build, at 0 (off), 2, 32 and 64.
-# usage: bash profiles/r05_cfg5.sh <outdir>
+# usage: bash profiles/r05/scripts/r05_cfg5.sh <outdir>
 set -o pipefail
 OUT=${1:-gpurun_out/r05_cfg5}
 mkdir -p $OUT

@@ -2,7 +2,7 @@
 # Round 5: config 5's time split ($CEP_PROF, measurement build) with the cooperative walk hops
 # off (0) and at 2 / 8 walkers, node pool chunks of 64 (default) and 1024 nodes per lane; one
 # batch of 125k keys, one timed push.
-# usage: bash profiles/r05_cfg5prof.sh <outdir> [configs "C:NC ..."]
+# usage: bash profiles/r05/scripts/r05_cfg5prof.sh <outdir> [configs "C:NC ..."]
 set -o pipefail
 OUT=${1:-gpurun_out/r05_cfg5prof}; shift
 CONFS=${@:-0:64 2:64 8:64}

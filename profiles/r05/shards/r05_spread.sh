@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: the world-8 shards (each alone) with their spread launch over more waves than the
 # chip holds at once ($CEP_SPREAD_WAVES, measurement build): fewer keys per wave.
-# usage: bash profiles/r05_spread.sh <outdir> [waves ...]
+# usage: bash profiles/r05/scripts/r05_spread.sh <outdir> [waves ...]
 OUT=${1:-gpurun_out/r05_spread}; shift
 mkdir -p $OUT
 for W in ${@:-0 6144 12288 24576}; do

@@ -758,6 +758,48 @@ def test_repeated_batch_allocates_nothing(query):
         check("arrival")
 
 
+@pytest.mark.gpu
+def test_sessions_interleaved_on_their_streams():
+    """ The conditions of the round-5 arrival-order flake, all at once: two
+    sessions on their own non-blocking streams - one taking arrival-order pushes (partition +
+    NFA), one stencil pushes that return without a host sync and are not read back between
+    pushes - interleaved with JSON decode + `[symbol]` keys on the default stream and a third
+    session's key-partitioned pushes.  Every result stays exactly what the same push gives alone."""
+    cfg = W.SynthConfig("t", "stock", 3000, 400, 0xCE90000 + 3)
+    off, cols = W.generate(cfg)
+    keys, acols = W.generate_arrival(cfg)
+    scfg = W.SynthConfig("t", "abc", 2000, 2000, 0xCE90000 + 2)
+    soff, scols = W.generate(scfg)
+    a = N.Session(N.Query(W.stock_query("readme").to_ir()))
+    b = N.Session(N.Query(W.strict_abc_query().to_ir()))
+    c = N.Session(N.Query(W.stock_query("readme").to_ir()))
+    a.push(off, cols)
+    want_a = a.digest(0)
+    b.push(soff, scols)
+    want_b = b.digest(0)
+    c.push(off, cols)
+    jcfg = W.SynthConfig("t", "stock", 300, 60, W.CONFIGS[3].seed)
+    jk, jc = W.generate_arrival(jcfg)
+    recs = [b'{"volume":%d,"price":%d,"name":"SYM%d"}' % (int(v), int(p), int(k)) for k, p, v in zip(jk, jc[0], jc[1])]
+    jb = N.StockJsonBatch.from_records(recs)
+    seen = []
+    for i in range(8):
+        a.push_arrival(keys, acols, cfg.n_keys)
+        b.push(soff, scols)  # (no read-back: its kernels may still run during what follows)
+        d = N.decode_stock_json(jb, 4)
+        sk, n_sym = N.symbol_keys(jb, d)
+        c.push(off, cols)
+        b.push(soff, scols)
+        got_a = a.digest(0)
+        got_c = c.digest(0)
+        ok_sym = n_sym == jcfg.n_keys and np.array_equal(sk.download(np.uint32, len(recs)), jk.astype(np.uint32))
+        seen.append((i, got_a == want_a, got_c == want_a, ok_sym, a.stats(0)["allocs"]))
+        if i % 2:
+            seen[-1] += (b.digest(0) == want_b,)
+    assert all(all(x for x in s[1:4]) and (s[4] == 0 or s[0] == 0) and (len(s) < 6 or s[5]) for s in seen), seen
+    assert b.digest(0) == want_b
+
+
 def test_arrival_generator_matches_numpy():
     cfg = W.SynthConfig("t", "stock", 300, 200, 77, key_base=5)
     st = N.synth_arrival_stream("stock", cfg.seed, cfg.n_keys, cfg.mean_events, cfg.key_base)

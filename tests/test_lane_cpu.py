@@ -12,6 +12,7 @@ import lane_cpu
 import oracle
 from fuzz_queries import random_query, random_stream
 from ref_queries import STOCK_KATS, STRING_KATS, build_case, kats
+from kafkastreams_cep_amd import native as N
 from kafkastreams_cep_amd import workloads as W
 
 KAT_CASES = [n for n in kats() if n in STRING_KATS or n in STOCK_KATS]
@@ -410,3 +411,64 @@ def test_lane_whole_wave_small_queue_retry(monkeypatch):
     g = lane_cpu.run(ir, off, cols, rcap=2)
     assert g["retried"] > 0
     lane_cpu.assert_same(g, oracle.run(ir, off, cols, threads=8), off)
+
+
+def _nullness_queries():
+    """fuzz queries whose generated step masks fold null bits (compile.cpp fold_nullness), plus
+    hand-made ones: skip_till_any branching with folds on both stages, getOrElse reads, and a
+    PROCEED chain of optional / zeroOrMore stages carrying folds"""
+    from kafkastreams_cep_amd import EventSchema, QueryBuilder
+    qs = []
+    for seed in range(0, 400):
+        q = random_query(seed)
+        ir = q.to_ir()
+        if oracle.compile_check(ir):
+            continue
+        if "static fold nullness" in N.Query(ir).jit_source:
+            qs.append((f"fuzz{seed}", ir, seed))
+        if len(qs) >= 10:
+            break
+    S = EventSchema({"a": "int", "b": "int"})
+    qb = QueryBuilder(S)
+    any2 = (qb.select("x").where(lambda k, v, ts, s: v.a > 2).fold("u", lambda k, v, c: v.a, type="int").then()
+            .select("y").oneOrMore().skipTillAnyMatch().where(lambda k, v, ts, s: v.b > s.get("u"))
+            .fold("u", lambda k, v, c: c + v.b, type="int").fold("w", lambda k, v, c: v.a * 2 - v.b, type="int").then()
+            .select("z").skipTillAnyMatch().where(lambda k, v, ts, s: v.a < s.getOrElse("w", 5)).build())
+    chain = (QueryBuilder(S).select("p").where(lambda k, v, ts, s: v.a >= 5).fold("u", lambda k, v, c: v.a, type="int")
+             .then().select("q").optional().skipTillNextMatch().where(lambda k, v, ts, s: v.b < s.getOrElse("u", 3))
+             .fold("w", lambda k, v, c: c + v.a, type="int").then()
+             .select("r").zeroOrMore().skipTillNextMatch().where(lambda k, v, ts, s: v.a > s.get("u"))
+             .fold("u", lambda k, v, c: c + v.b, type="int").then()
+             .select("t").where(lambda k, v, ts, s: v.b != s.getOrElse("w", 1)).build())
+    qs += [("any_two_stage_folds", any2.to_ir(), 7), ("proceed_chain", chain.to_ir(), 11)]
+    return qs
+
+
+@pytest.mark.parametrize("name,ir,seed", _nullness_queries())
+def test_lane_static_fold_nullness_is_exact(name, ir, seed):
+    """ the static fold nullness masks (`w.nm &= ...` at each dispatch case) change
+    nothing: the generated step with and without them gives the same matches and the same
+    exceptions on the same streams, both equal to the oracle."""
+    src = N.Query(ir).jit_source
+    masked = [ln for ln in src.splitlines() if "static fold nullness" in ln]
+    if not masked and name.startswith("fuzz"):
+        pytest.skip("no mask generated")
+    plain = "\n".join(ln for ln in src.splitlines() if "static fold nullness" not in ln) + "\n"
+    off, cols = random_stream(seed, 80, 16)
+    r = oracle.run(ir, off, cols)
+    a = lane_cpu.run(ir, off, cols)
+    b = _run_source(ir, plain, off, cols)
+    lane_cpu.assert_same(a, r, off)
+    lane_cpu.assert_same(b, r, off)
+
+
+def _run_source(ir, source, off, cols):
+    """lane_cpu.run on an explicit kernel source (a single query: the group path of run() with a
+    one-member plan)"""
+    g = {"source": source, "members": [0], "literals": np.zeros((1, 0), np.int64)}
+    m = lane_cpu.run(ir, off, cols, _group=g)
+    key_off = np.asarray(off, np.uint64)
+    m["emit_pos"] = (key_off[m["key"].astype(np.int64) % (len(key_off) - 1)] + m["emit_seq"]).astype(np.uint64)
+    pk = np.repeat(m["key"].astype(np.int64) % (len(key_off) - 1), np.diff(m["pair_off"].astype(np.int64)))
+    m["pair_pos"] = (key_off[pk] + m["pair_seq"]).astype(np.uint64)
+    return m

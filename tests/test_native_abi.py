@@ -153,3 +153,18 @@ def test_release_build_reads_only_jit_cache():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+def test_no_stream_ordered_or_null_stream_allocation():
+    """ The library allocates device memory with hipMalloc only - no
+    stream-ordered pool (hipMallocAsync / hipFreeAsync) anywhere - and the session paths copy on
+    the session's own stream (no null-stream hipMemcpy outside cep_memcpy, which waits for the
+    device first)."""
+    import subprocess
+    so = os.path.join(ROOT, "kafkastreams-cep_amd", "libcep.so")
+    syms = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
+    for bad in ("hipMallocAsync", "hipFreeAsync", "hipMallocFromPoolAsync", "hipMemPool"):
+        assert bad not in syms, bad
+    csrc = os.path.join(ROOT, "kafkastreams-cep_amd", "csrc")
+    ses = re.sub(r"//.*", "", open(os.path.join(csrc, "session.cpp")).read())
+    assert len(re.findall(r"hipMemcpy\(", ses)) == 1  # cep_memcpy's, after hipDeviceSynchronize
+    assert "hipDeviceSynchronize());\n    HIPCHECK(hipMemcpy(dst, src, bytes, k))" in ses

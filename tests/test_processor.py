@@ -12,6 +12,7 @@
 The CPU tests run the processor's host logic over an oracle-backed stand-in for the device
 session (tests/proc_fake.py); the `gpu` tests run the same cases through libcep.so.
 """
+import base64
 import json
 
 import numpy as np
@@ -372,7 +373,7 @@ def test_checkpoint_is_plain_data():
     assert blob[:8] == b"CEPPROC2"
     n = int.from_bytes(blob[8:16], "little")
     host = json.loads(blob[16 + n:].decode())
-    assert host["version"] == 2 and len(host["keys"]) == len(host["events"]) == len(host["base"])
+    assert host["version"] == 3 and len(host["keys"]) == len(host["events"]) == len(host["base"])
     proc2 = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
     proc2.init(P.RecordContext("StockEvents", 0, stores=stores))
     assert [[(e.offset, e.value) for e in evs] for evs in proc2._events] == \
@@ -431,6 +432,39 @@ def test_json_serde_keeps_types():
     assert np.isnan(P.JsonSerde.deserialize(P.JsonSerde.serialize(float("nan"))))
     with pytest.raises(TypeError):
         P.JsonSerde.serialize({1, 2})
+
+
+def test_checkpoint_version2_reads_plain_json():
+    """ host-half version 3 is the tagged JsonSerde encoding; a version-2 blob (plain
+    JSON values) still restores, and a value dict holding a "__cep__" key comes back as data."""
+    import json
+    stores = {}
+    ctx = P.RecordContext("StockEvents", 0, stores=stores)
+    proc = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
+    proc.init(ctx)
+    recs = _readme_records()
+    for k, v, ts in recs[:3]:
+        ctx.send(k, dict(v, tag={"__cep__": "x"}), ts)
+    proc.punctuate(0)
+    blob = stores[P.NFA_STATES_STORE][("StockEvents", 0)]
+    n = int.from_bytes(blob[8:16], "little")
+    host = json.loads(blob[16 + n:].decode())
+    assert host["version"] == 3
+    # rewrite the host half as version 2 wrote it: values as plain JSON
+    host["version"] = 2
+    host["events"] = [[[ts, t, pa, off, base64.b64encode(json.dumps(P.JsonSerde.deserialize(base64.b64decode(v))).encode()).decode()]
+                       for ts, t, pa, off, v in evs] for evs in host["events"]]
+    host["keys"] = [base64.b64encode(json.dumps(P.JsonSerde.deserialize(base64.b64decode(k))).encode()).decode()
+                    for k in host["keys"]]
+    old = blob[:16 + n] + json.dumps(host).encode()
+    proc2 = P.CEPProcessor(W.stock_query("readme"), batch_size=4, session_factory=OracleStreamSession)
+    proc2.init(P.RecordContext("StockEvents", 0, stores={}))
+    proc2.restore(old)
+    assert [[e.value for e in evs] for evs in proc2._events] == [[e.value for e in evs] for evs in proc._events]
+    assert proc2._events[0][0].value["tag"] == {"__cep__": "x"}
+    host["version"] = 1
+    with pytest.raises(ValueError):
+        proc2.restore(blob[:16 + n] + json.dumps(host).encode())
 
 
 @pytest.mark.parametrize("user_serde", [False, True])
