@@ -134,7 +134,7 @@ inline std::string jit_stream_source(const std::string& src) {
   int pairs = 3, layout = 6, plog = 1;
   tuning_stream_build(&pairs, &layout, &plog);
   return "#define CEP_DEWEY_PAIRS " + std::to_string(pairs) + "\n#define CEP_LAYOUT_PAIRS " + std::to_string(layout) +
-         "\n#define CEP_PUT_LOG " + std::to_string(plog) + "\n#define CEP_STREAM_STOP 1\n"
+         "\n#define CEP_PUT_LOG " + std::to_string(plog) + "\n#define CEP_STREAM_STOP 1\n#define CEP_WALK_IN_PLACE 0\n"
          "#define CEP_PERSIST_LANES 0\n#define CEP_WAVES_EU 3\n" + src;
 }
 struct Cols;

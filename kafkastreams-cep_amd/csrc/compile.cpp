@@ -663,6 +663,8 @@ static std::string generate_jit(const cep_query* q, const Builder& b, LitCtx& li
   // the narrow build re-runs deferred-walk conflicts in the wide one instead of carrying the
   // put log (nfa_lane.h kPutLog)
   o += "#ifndef CEP_PUT_LOG\n#define CEP_PUT_LOG 0\n#endif\n";
+  // ... and always defers its walks: the in-place path left out (nfa_lane.h CEP_WALK_IN_PLACE)
+  o += "#ifndef CEP_WALK_IN_PLACE\n#define CEP_WALK_IN_PLACE 0\n#endif\n";
   // a single query's narrow build never runs persistent lanes (session.cpp: only kernel groups
   // and the re-runs, which take the wide build, do): its kernel holds run() alone, half the code
   if (!lits.param) o += "#ifndef CEP_PERSIST_LANES\n#define CEP_PERSIST_LANES 0\n#endif\n";

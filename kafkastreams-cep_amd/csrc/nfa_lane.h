@@ -146,6 +146,15 @@ constexpr uint32_t kWalkHint = 8;
 #ifndef CEP_PUT_LOG
 #define CEP_PUT_LOG 1
 #endif
+// Walks in place (A.defer == 0): the wide build's re-runs after a put log overflowed, and the
+// interpreter's.  The narrow and stream builds are never launched with A.defer == 0 (session.cpp:
+// their re-runs and continuations take the wide build) and leave the path out: inlined into
+// every walk site of the step, its dead code alone made the record loop spill 15 VGPRs at the
+// 168-VGPR budget of 3 waves per SIMD (with it out: 163 VGPRs, none spilled).  (Launched with
+// A.defer == 0 anyway, such a build defers: exact, a conflict re-runs the job in the wide build.)
+#ifndef CEP_WALK_IN_PLACE
+#define CEP_WALK_IN_PLACE 1
+#endif
 // a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
 // re-runs the job in the wide one (a retry); the wide build's limit is final
 #ifndef CEP_STREAM_STOP
@@ -715,7 +724,7 @@ struct Lane {
   __device__ __forceinline__ void walk(uint32_t flags, uint32_t sk, uint32_t ev, uint32_t first, const Dewey& v0,
                                       uint32_t hint = CEP_NONE) {
     CEP_STAT(2);
-    if (!A.defer) {  // (in place: hints are not kept valid)
+    if (CEP_WALK_IN_PLACE && !A.defer) {  // (in place: hints are not kept valid)
       walk_now(flags, sk, ev, first, v0, j);
       return;
     }

@@ -28,7 +28,7 @@ _libs = {}
 # session.cpp's stream build (cep_internal.h jit_stream_source; the lane driver keeps its own
 # persistent-lane setting)
 STREAM_PREFIX = ("#define CEP_DEWEY_PAIRS 3\n#define CEP_LAYOUT_PAIRS 6\n#define CEP_PUT_LOG 1\n"
-                 "#define CEP_STREAM_STOP 1\n#define CEP_WAVES_EU 3\n")
+                 "#define CEP_STREAM_STOP 1\n#define CEP_WALK_IN_PLACE 0\n#define CEP_WAVES_EU 3\n")
 
 
 def build(ir: bytes, source: str | None = None, narrow: bool = False, stream: bool = False):
@@ -41,7 +41,11 @@ def build(ir: bytes, source: str | None = None, narrow: bool = False, stream: bo
     src = re.sub(r"__attribute__\(\(amdgpu_waves_per_eu\(\w+\)\)\)", "", source or N.Query(ir).jit_source)
     if stream:
         src = STREAM_PREFIX + src
-    elif not narrow:
+    elif narrow:
+        # (this driver re-runs a narrow job's walk conflicts in the same build with walks in
+        # place; libcep re-runs them in the wide build, so its narrow build leaves that path out)
+        src = "#define CEP_WALK_IN_PLACE 1\n" + src
+    else:
         src = "#define CEP_DEWEY_PAIRS 6\n" + src
     # $CEP_LANE_DEFINES="A=1 B=2": tuning knobs of nfa_lane.h for this build (tests of the knobs)
     src = "".join(f"#define {d.replace('=', ' ', 1)}\n" for d in os.environ.get("CEP_LANE_DEFINES", "").split()) + src
