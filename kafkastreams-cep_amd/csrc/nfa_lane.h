@@ -155,6 +155,11 @@ constexpr uint32_t kWalkHint = 8;
 #ifndef CEP_WALK_IN_PLACE
 #define CEP_WALK_IN_PLACE 1
 #endif
+// a value every active lane of the wave holds (the compiler then branches on it with the scalar
+// unit); the CPU lane build runs lanes one at a time and takes the lane's own
+#ifndef CEP_UNIFORM
+#define CEP_UNIFORM(x) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(x)))
+#endif
 // a Dewey version outgrowing the pairs this build holds: the narrow build (fewer than 6)
 // re-runs the job in the wide one (a retry); the wide build's limit is final
 #ifndef CEP_STREAM_STOP
@@ -331,8 +336,23 @@ struct Lane {
 
   // ---------------------------------------------------------------- records
   // `pf`: node chain that resolves a pending ev_first (the event the record was made at)
+  // (`slot` is wave-uniform at every call - the queue loops step record i of every lane together -
+  // so one scalar branch picks LDS or HBM for all of the record's quads and their loads go out
+  // together: a choice per quad on a slot the compiler takes for divergent cost a wait each)
   __device__ __forceinline__ void load(uint32_t h, uint32_t slot, Rec<F>& r, uint32_t pf, v4u* raw = nullptr) const {
-    const v4u hd = rd(h, slot, 0);
+    const bool lds = kRL > 0 && CEP_UNIFORM(slot) < kRL;
+    v4u hd, d0, fqs[Lay::kFoldQuads];
+    if (lds) {
+      hd = *LQ(h, slot, 0);
+      d0 = *LQ(h, slot, 1);
+#pragma unroll
+      for (int k = 0; k < Lay::kFoldQuads; k++) fqs[k] = *LQ(h, slot, Lay::lds_quad(1 + Lay::kDwQuads + k));
+    } else {
+      hd = *QP(h, slot, 0);
+      d0 = *QP(h, slot, 1);
+#pragma unroll
+      for (int k = 0; k < Lay::kFoldQuads; k++) fqs[k] = *QP(h, slot, 1 + Lay::kDwQuads + k);
+    }
     if (raw) *raw = hd;
     r.stage = hd.x & kStageMask;
     r.event = hd.y;
@@ -341,8 +361,9 @@ struct Lane {
     r.ver.n = hd.x >> 24;
 #pragma unroll
     for (int k = 0; k < Lay::kDwRegQuads; k++) {
-      v4u dq = {0, 0, 0, 0};
-      if ((uint32_t)(2 * k) < r.ver.n) dq = rd(h, slot, 1 + k);
+      // (pairs past the first two: HBM at every slot, and only when the version has them)
+      v4u dq = d0;
+      if (k > 0) dq = (uint32_t)(2 * k) < r.ver.n ? *QP(h, slot, 1 + k) : v4u{0, 0, 0, 0};
       r.ver.v[2 * k] = (int32_t)dq.x;
       r.ver.c[2 * k] = dq.y;
       if (2 * k + 1 < kDeweyPairs) {
@@ -358,7 +379,7 @@ struct Lane {
     uint32_t w[Lay::kFoldQuads * 4];
 #pragma unroll
     for (int k = 0; k < Lay::kFoldQuads; k++) {
-      const v4u fq = rd(h, slot, 1 + Lay::kDwQuads + k);
+      const v4u fq = fqs[k];
       w[4 * k] = fq.x;
       w[4 * k + 1] = fq.y;
       w[4 * k + 2] = fq.z;
@@ -373,13 +394,24 @@ struct Lane {
   __device__ __forceinline__ void store_head(uint32_t h, uint32_t slot, uint32_t stage, uint32_t event,
                                              uint32_t ev_first, const Dewey& ver0, uint32_t node, uint32_t flags = 0) {
     const Dewey ver = dw_pin(ver0);
-    wr(h, slot, 0, v4u{stage | flags | (ver.n << 24), event, ev_first, node});
+    // the header and the first pairs: one branch for both (LDS slot or HBM), then pairs past the
+    // first two (HBM at every slot)
+    const v4u q0 = v4u{stage | flags | (ver.n << 24), event, ev_first, node};
+    const v4u q1 = v4u{(uint32_t)ver.v[0], ver.c[0], 1 < kDeweyPairs ? (uint32_t)ver.v[1 < kDeweyPairs ? 1 : 0] : 0u,
+                       1 < kDeweyPairs ? ver.c[1 < kDeweyPairs ? 1 : 0] : 0u};
+    if (kRL > 0 && slot < kRL) {
+      *LQ(h, slot, 0) = q0;
+      *LQ(h, slot, 1) = q1;
+    } else {
+      *QP(h, slot, 0) = q0;
+      *QP(h, slot, 1) = q1;
+    }
 #pragma unroll
-    for (int k = 0; k < Lay::kDwRegQuads; k++)
+    for (int k = 1; k < Lay::kDwRegQuads; k++)
       if ((uint32_t)(2 * k) < ver.n)
-        wr(h, slot, 1 + k, v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
-                               2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
-                               2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u});
+        *QP(h, slot, 1 + k) = v4u{(uint32_t)ver.v[2 * k], ver.c[2 * k],
+                                  2 * k + 1 < kDeweyPairs ? (uint32_t)ver.v[2 * k + 1] : 0u,
+                                  2 * k + 1 < kDeweyPairs ? ver.c[2 * k + 1] : 0u};
   }
 
   __device__ __forceinline__ void store_folds(uint32_t h, uint32_t slot, const int64_t* v, uint32_t nm) {
@@ -396,9 +428,15 @@ struct Lane {
         w[3 + 2 * s] = (uint32_t)((uint64_t)v[s] >> 32);
       }
     }
+    if (kRL > 0 && slot < kRL) {
 #pragma unroll
-    for (int k = 0; k < Lay::kFoldQuads; k++)
-      wr(h, slot, 1 + Lay::kDwQuads + k, v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]});
+      for (int k = 0; k < Lay::kFoldQuads; k++)
+        *LQ(h, slot, Lay::lds_quad(1 + Lay::kDwQuads + k)) = v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < Lay::kFoldQuads; k++)
+        *QP(h, slot, 1 + Lay::kDwQuads + k) = v4u{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+    }
   }
 
   // (a record moved to another slot: its twin flags do not hold there)
@@ -794,6 +832,9 @@ struct Lane {
     P.n1 = gn[1];
     P.f0 = gp[0];
     P.f1 = gp[1];
+    // (all four in flight before the step branches on any: otherwise the compiler sinks the
+    // pointer loads into the live-node branch, a second dependent round trip per hop)
+    asm volatile("" : "+v"(P.n0), "+v"(P.n1), "+v"(P.f0), "+v"(P.f1));
   }
 
   // One node of a walk at node s with walker version w.  Returns false when the walk ends (or

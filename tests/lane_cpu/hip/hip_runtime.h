@@ -24,6 +24,8 @@
 #define __shared__ static  // the block's LDS: one static array (its waves run one after another)
 #define CEP_LDS_AS           // (no address spaces on the host)
 #define asm(...) ((void)0)
+// (lanes run one at a time: a wave-uniform value is the lane's own)
+#define CEP_UNIFORM(x) ((uint32_t)(x))
 
 // (the vector types the generated bitmap kernel's 16-B loads use)
 struct int4 {
