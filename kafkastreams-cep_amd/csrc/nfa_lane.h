@@ -314,6 +314,12 @@ struct Lane {
   __device__ __forceinline__ bool lds_slot(uint32_t slot, int quad) const {
     return kRL > 0 && Lay::in_lds(quad) && slot < kRL;
   }
+  // quad `quad` of a slot every active lane of the wave reads at once (the queue loops): the
+  // LDS-or-HBM choice on the scalar unit
+  __device__ __forceinline__ v4u rd_u(uint32_t h, uint32_t slot, int quad) const {
+    if (kRL > 0 && Lay::in_lds(quad) && CEP_UNIFORM(slot) < kRL) return *LQ(h, slot, Lay::lds_quad(quad));
+    return *QP(h, slot, quad);
+  }
   __device__ __forceinline__ v4u rd(uint32_t h, uint32_t slot, int quad) const {
     if (lds_slot(slot, quad)) return *LQ(h, slot, Lay::lds_quad(quad));
     return *QP(h, slot, quad);
@@ -439,11 +445,12 @@ struct Lane {
     }
   }
 
-  // (a record moved to another slot: its twin flags do not hold there)
+  // (a record moved to another slot: its twin flags do not hold there; `from` is wave-uniform:
+  // the finals' compaction steps slot i of every lane together)
   __device__ __forceinline__ void copy_rec(uint32_t h, uint32_t from, uint32_t to) {
 #pragma unroll
     for (int k = 0; k < Lay::kQuads; k++) {
-      v4u q4 = rd(h, from, k);
+      v4u q4 = rd_u(h, from, k);
       if (k == 0) q4.x &= ~(kTwin | kTwinT);
       wr(h, to, k, q4);
     }
@@ -573,12 +580,13 @@ struct Lane {
       err = KE_RETRY;
       return;
     }
+    // (both quads of the node read together, written whole: it is a node of the current event,
+    // which no queued walk reads before the next flush)
+    const v4u q0 = *NQ(node, 0), q1 = *NQ(node, 1);  // {event, refs, head, tail}, {same_next, meta, lk, key}
     write_pred(p, prev, v);
-    Node& n = A.nodes[node];
-    if (n.head == CEP_NONE) n.head = p;
-    else PR(n.tail).next = p;
-    n.tail = p;
-    n.meta += 1u << 16;
+    if (q0.z != CEP_NONE) PR(q0.w).next = p;
+    *NQ(node, 0) = v4u{q0.x, q0.y, q0.z == CEP_NONE ? p : q0.z, p};
+    *NQ(node, 1) = v4u{q1.x, q1.y + (1u << 16), q1.z, q1.w};
   }
 
   // put(stage, evt, version)  KVSharedVersionedBuffer.java:117-128 (overwrites)
@@ -637,7 +645,7 @@ struct Lane {
   // a flush (walks may delete nodes): the queued records' node hints no longer hold
   __device__ __forceinline__ void clear_hints() {
     for (uint32_t i = 0; i < count; i++) {
-      v4u hd = rd(half, i, 0);
+      v4u hd = rd_u(half, i, 0);
       if (hd.w != CEP_NONE) {
         hd.w = CEP_NONE;
         hd.x &= ~(kTwin | kTwinT);  // (changed in place: no longer its twin's copy)
@@ -1047,8 +1055,9 @@ struct Lane {
         w.len = h.w;
 #pragma unroll
         for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
+          // (quad 0 with the header: an entry's version has a pair)
           v4u d = {0, 0, 0, 0};
-          if ((uint32_t)(2 * k) < w.n) d = *WQ(qs, 1 + k);
+          if (k == 0 || (uint32_t)(2 * k) < w.n) d = *WQ(qs, 1 + k);
           w.v[2 * k] = (int32_t)d.x;
           w.c[2 * k] = d.y;
           if (2 * k + 1 < kDeweyPairs) {
@@ -1195,7 +1204,7 @@ struct Lane {
     // matchConstruction: finals in order, then drop them from the queue
     uint32_t w = 0;
     for (uint32_t i = 0; i < count; i++) {
-      const v4u hd = rd(oh, i, 0);
+      const v4u hd = rd_u(oh, i, 0);
       if (hd.x & kRecFinal) {
         Rec<F> r;
         load(oh, i, r, cur_first);

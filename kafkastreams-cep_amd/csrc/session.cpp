@@ -681,6 +681,8 @@ void run_nfa(cep_session* s, GroupRt& g) {
   launches++;
   Scratch h{};
   HIPCHECK(hipMemcpyAsync(&h, sc, sizeof h, hipMemcpyDeviceToHost, s->stream));
+  uint32_t tops[2] = {0, 0};  // a stream's pool tops, read back with the counters (one wait)
+  if (streaming) HIPCHECK(hipMemcpyAsync(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
   if (wm_here) s->watermark = (int64_t)(h.wmax ^ 0x8000000000000000ull);
   if (prof) {  // one line per launch on stderr: the counters of nfa_lane.h's CEP_PROF list
@@ -731,8 +733,7 @@ void run_nfa(cep_session* s, GroupRt& g) {
     }
   }
   if (streaming) {  // no re-runs: a key that hit a limit keeps its error (sticky, reported)
-    uint32_t tops[2];
-    copy_sync(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost, s->stream);
+    if (widened) copy_sync(tops, S.tops.p, sizeof tops, hipMemcpyDeviceToHost, s->stream);  // (moved on)
     S.node_used = (uint32_t)std::min<uint64_t>(tops[0], S.node_cap);
     S.pred_used = (uint32_t)std::min<uint64_t>(tops[1], S.pred_cap);
     h.n_cap_err = 0;
