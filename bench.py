@@ -78,7 +78,9 @@ class Dist:
             import torch
             import torch.distributed as dist
 
-            self.backend = backend or "nccl"
+            # ($CEP_BENCH_BACKEND=gloo with $CEP_BENCH_DEVICE=0: a rehearsal of the N-rank path
+            # on a one-GPU box, every rank on the same card, the collectives on the CPU)
+            self.backend = backend or os.environ.get("CEP_BENCH_BACKEND", "nccl")
             self.device = "cuda" if self.backend == "nccl" else "cpu"
             if self.device == "cuda":
                 torch.cuda.set_device(self.local)
@@ -672,7 +674,7 @@ def main():
     dist = Dist()
     if dist.world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={dist.world}", file=sys.stderr)
-    device = dist.local
+    device = int(os.environ.get("CEP_BENCH_DEVICE", dist.local))
     strong = args.scaling == "strong"
     key_base = 0 if strong else dist.rank * args.keys
     cfg = W.SynthConfig("cfg3_stock", "stock", args.keys, args.mean, W.CONFIGS[3].seed, key_base=key_base)

@@ -3,7 +3,7 @@
 # per record load, one branch per record store, a walk step's four loads in flight together):
 # the GPU suite, the headline figure, occupancy variants, the world-8 shards at 3 and 2 waves
 # per SIMD, and the config 4 stress / config 5 / streaming workloads on their own.
-# usage: bash profiles/r06/scripts/r06_walk.sh <outdir> [parts: tests quick occ shards work]
+# usage: bash profiles/r06/scripts/r06_walk.sh <outdir> [parts: tests quick occ shards dist work]
 set -o pipefail
 OUT=${1:-gpurun_out/r06_walk}; shift
 PARTS=${@:-tests quick occ shards work}
@@ -22,6 +22,14 @@ for P in $PARTS; do
       ;;
     shards)
       CEP_MEASURE=1 CEP_JIT_WAVES=2 timeout -k 10 300 python -u profiles/workload.py shards --steps 2 > $OUT/shards_w2.json 2> $OUT/shards_w2.log || exit $?
+      ;;
+    dist)
+      # the N-rank bench path rehearsed on this one GPU: every rank on cuda:0, the collectives
+      # over gloo (the driver's N > 1 runs use RCCL, one rank per GPU); the union of the ranks'
+      # checksums must equal the one-GPU checksum
+      for NP in 2 4; do
+        CEP_BENCH_BACKEND=gloo CEP_BENCH_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP --master-addr 127.0.0.1 --master-port $((29510 + NP)) bench.py --gpus $NP --steps 3 --warmup 1 > $OUT/dist_n$NP.json 2> $OUT/dist_n$NP.log || exit $?
+      done
       ;;
     work)
       timeout -k 10 300 python -u profiles/workload.py cfg4s --steps 2 > $OUT/cfg4s.json 2> $OUT/cfg4s.log || exit $?
