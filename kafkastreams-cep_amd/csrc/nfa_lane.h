@@ -263,8 +263,6 @@ struct Lane {
   // in_info: its Dewey length (bits 0-15; a longer one never matches) | its stored twin flags |
   // kInPend (stored ev_first kPending)
   uint32_t in_slot = CEP_NONE, pend_slot = CEP_NONE, in_info = 0;
-  bool inplace = true;  // every output of this event so far a keep at its own slot (push_rec)
-  uint32_t kept_n = 0;  // !inplace: the records kept in place before the event stopped being so
   uint32_t cur_first = CEP_NONE;  // node chain of event j
   uint32_t pf_ev = CEP_NONE;      // node chain of the previous event (resolves kPending)
   int err = KE_OK;
@@ -447,18 +445,6 @@ struct Lane {
     }
   }
 
-  // the records kept in place at slots [0, n) of the input half, to the same slots of the output
-  // half (an event that stopped being in place, push_rec); their twin flags are dropped
-  __device__ __forceinline__ void move_kept(uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) {
-#pragma unroll
-      for (int k = 0; k < Lay::kQuads; k++) {
-        v4u q4 = rd(half, i, k);
-        if (k == 0) q4.x &= ~(kTwin | kTwinT);
-        wr(half ^ 1u, i, k, q4);
-      }
-    }
-  }
   // (a record moved to another slot: its twin flags do not hold there; `from` is wave-uniform:
   // the finals' compaction steps slot i of every lane together)
   __device__ __forceinline__ void copy_rec(uint32_t h, uint32_t from, uint32_t to) {
@@ -495,22 +481,6 @@ struct Lane {
     const uint32_t slot = ocount++;
     const uint32_t ef = (event == j && ev_first == CEP_NONE) ? kPending : ev_first;
     if (stage & kRecFinal) n_final++;
-    // In-place events (`inplace`, event_pre): while every record of the event so far was re-added
-    // as it is at its own slot (an IGNORE without a new stage, NFA.java:225 - 92 % of config 3's
-    // record steps), the output queue is the input queue itself: such a keep writes nothing (its
-    // header only when its stored ev_first was still kPending, resolved in place) and the event
-    // does not swap halves.  From the first output that is anything else the event goes on
-    // double-buffered; the records kept so far move to the output half at the event's end
-    // (event_post: move_kept, one copy of the code) - nothing writes their slots before it.
-    if (inplace) {
-      if (keep && slot == in_slot && ver.len == (in_info & 0xFFFFu)) {
-        if (in_info & kInPend) wr(half, slot, 0, v4u{stage | (ver.n << 24), event, ef, node});  // (twin flags dropped)
-        pend_slot = slot;  // (its folds are in place too: set_folds writes nothing)
-        return (int)slot;
-      }
-      kept_n = slot;
-      inplace = false;
-    }
     // (on the keep path the stage word, event and node hint are the record's own - sw is its
     // stage word with its own branching flag - so the head differs from the stored one only
     // when the stored ev_first was kPending: in_info bit kInPend)
@@ -1169,7 +1139,6 @@ struct Lane {
     cur_first = CEP_NONE;
     n_final = 0;
     ocount = 0;
-    inplace = true;
     // prefetch the next event's fields (consumed by the next event)
     nev = ev;
     nmore = j + 1 < j0 + n_ev;
@@ -1220,8 +1189,7 @@ struct Lane {
     }
     CEP_PT(te2);
     CEP_PACC(3, te2 - te1);
-    if (!inplace && kept_n) move_kept(kept_n);
-    const uint32_t oh = inplace ? half : half ^ 1u;  // (an in-place event keeps its half)
+    const uint32_t oh = half ^ 1u;
     half = oh;
     count = ocount;
     if (nmore) {
