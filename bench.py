@@ -567,7 +567,7 @@ def end_to_end(args, device, dist):
                       "retried_jobs": int(b["retried_jobs"]), "allocs": int(b["allocs"])})
     N.lib().cep_sync(s.h)
     el = time.perf_counter() - t0
-    n_m, _ = s.digest(0)
+    n_m, dig = s.digest(0)
     try:
         bal, _ = s.lane_balance(0)
     except N.CepError:
@@ -579,7 +579,7 @@ def end_to_end(args, device, dist):
             "partition_ms": mean("partition_ms"), "nfa_kernel_ms": mean("nfa_kernel_ms"), "main_ms": mean("main_ms"),
             "est_order_bits_ms": mean("est_order_bits_ms"), "retry_ms": mean("retry_ms"),
             "retried_jobs": sum(x["retried_jobs"] for x in steps), "allocs": sum(x["allocs"] for x in steps),
-            "lane_balance": bal, "per_step": steps, "matches_per_step": n_m}
+            "lane_balance": bal, "per_step": steps, "matches_per_step": n_m, "checksum": f"{dig:016x}"}
 
 
 def ingest(device, steps, keys, cpu_sample):

@@ -718,6 +718,37 @@ def test_arrival_order_batch(query):
     assert_parity(g, oracle.run(ir, off, cols, threads=8), off)
 
 
+@pytest.mark.parametrize("shape", ["round_robin", "sorted", "one_key", "random", "runs", "tiny"])
+def test_partition_shapes(shape):
+    """The onesweep partition (partition.hip: one count pass, a tile look-back per pass) against
+    numpy's stable argsort, on key orders that take every path of its counting and ranking: keys
+    arriving round-robin over 300k keys (3 passes of 7 bits; a wave's high digits all equal),
+    sorted (every wave's digits equal), a single key, random, long runs of one key, and a
+    batch smaller than one wave."""
+    rng = np.random.default_rng(11)
+    n_keys = {"round_robin": 300_000, "sorted": 70_000, "one_key": 5_000, "random": 1 << 20, "runs": 4_096,
+              "tiny": 300}[shape]
+    n = {"tiny": 37}.get(shape, 6_000_000)
+    if shape == "round_robin":
+        keys = (np.arange(n, dtype=np.int64) % n_keys).astype(np.uint32)
+    elif shape == "sorted":
+        keys = np.sort(rng.integers(0, n_keys, n)).astype(np.uint32)
+    elif shape == "one_key":
+        keys = np.full(n, n_keys - 1, np.uint32)
+    elif shape == "runs":
+        keys = np.repeat(rng.integers(0, n_keys, n // 1000 + 1), 1000)[:n].astype(np.uint32)
+    else:
+        keys = rng.integers(0, n_keys, n).astype(np.uint32)
+    vals = rng.integers(0, 16, n).astype(np.int32)
+    s = N.Session(N.Query(W.strict_abc_query().to_ir()))
+    s.push_arrival(keys, [vals], n_keys)
+    ko, arrival, _ = s.layout()
+    want = np.zeros(n_keys + 1, np.uint64)
+    np.cumsum(np.bincount(keys, minlength=n_keys), out=want[1:])
+    np.testing.assert_array_equal(ko, want)
+    np.testing.assert_array_equal(arrival, np.argsort(keys, kind="stable"))
+
+
 @pytest.mark.parametrize("query", ["readme", "strict"])
 def test_repeated_batch_allocates_nothing(query):
     """ A session pushed a batch of the shape it has already seen reuses
