@@ -17,7 +17,10 @@ from kafkastreams_cep_amd import workloads as W  # noqa: E402
 
 KNOBS = ("CEP_RING_LDS", "CEP_JIT_WAVES", "CEP_WALK_FLUSH", "CEP_QUIET_CHUNK", "CEP_JOB_DRAIN", "CEP_NO_PERSIST",
          "CEP_DEWEY_PAIRS", "CEP_RING_LDS_SLOTS", "CEP_STREAM_PAIRS",
-         "CEP_STREAM_LAYOUT", "CEP_STREAM_PUTLOG")
+         "CEP_STREAM_LAYOUT", "CEP_STREAM_PUTLOG", "CEP_PARTIAL_DRAIN",
+         # (session knobs, read at session creation)
+         "CEP_NODE_CHUNK", "CEP_OUT_CHUNK", "CEP_WALK_CAP", "CEP_RESIDENT_WAVES")
+SESSION_KNOBS = ("CEP_NODE_CHUNK", "CEP_OUT_CHUNK", "CEP_WALK_CAP", "CEP_RESIDENT_WAVES")
 DEFAULT = "default=;nolds=CEP_RING_LDS:0;w2=CEP_JIT_WAVES:2"
 
 
@@ -41,7 +44,9 @@ def query(name, env, variant):
               W.any_kleene_query(carry_volume=True).to_ir() if variant == "anys" else W.stock_query(variant).to_ir())
     q = N.Query(ir)
     for k in KNOBS:
-        if not k.startswith("CEP_STREAM_"):  # (read again when a streaming session builds its kernel)
+        # (CEP_STREAM_*: read again when a streaming session builds its kernel; the session
+        # knobs when the session is created - main() drops them after the variant's run)
+        if not k.startswith("CEP_STREAM_") and k not in SESSION_KNOBS:
             os.environ.pop(k, None)
     return q
 
