@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, onesweep partition (partition.hip: one count pass, per-pass tile look-back): the GPU
+# Round 6, partition variants (first the onesweep form, then the prefetching gather): the GPU
 # suite, the bench with the arrival-order end-to-end figure, and its kernel trace.
 # usage: bash profiles/r06/scripts/r06_part.sh <outdir> [parts: tests bench trace]
 set -o pipefail
