@@ -205,6 +205,22 @@ def test_full_size_digest_matches_oracle(query):
         assert f"{got[1]:016x}" == "a81bb860df5becf5"
 
 
+def test_shard_rank2_bit_exact():
+    """ The slowest world-8 shard of the headline stream at its full size:
+    the ~125k keys Kafka's partitioner gives rank 2 (murmur2(key) % 8), ~125M events - the
+    underfilled launch the projected scaling times (every wave resident, the heaviest keys
+    spread over the wave slots) - every match and exception equal to the oracle's."""
+    from kafkastreams_cep_amd import shard as SH
+    cfg = W.CONFIGS[3]
+    keys = np.nonzero(SH.partition_of(np.arange(cfg.n_keys, dtype=np.uint32), 8) == 2)[0]
+    assert 120_000 < len(keys) < 130_000
+    off, cols = W.generate(cfg, keys)
+    ir = W.stock_query("readme").to_ir()
+    r = oracle.run(ir, off, cols, threads=16)
+    assert r["n_matches"] > 50_000
+    assert_parity(gpu_run(ir, off, cols), r, off)
+
+
 def test_cfg3_streaming_medium_bit_exact():
     """ The streaming path the processor runs, at scale against the oracle
     instead of the GPU's own per-batch checksum: config 3 at 20k keys (every 50th key of the
@@ -257,6 +273,29 @@ def test_cfg5_medium_bit_exact():
     s.push(off, cols)  # a second batch of the same session (pools sized from the first)
     for i, r in enumerate(want):
         assert_parity(session_result(s, i, off), r, off)
+
+
+def test_cfg5_20k_keys_digest():
+    """ Config 5's kernel group at ten times the medium test's keys: 20k keys
+    of the BASELINE stream (every 50th, 20M events) x 64 queries in one launch per batch - per
+    query the match count, the checksum over every (key, emission, pairs) and the keys with an
+    exception equal the oracle's."""
+    cfg = W.CONFIGS[3]
+    off, cols = W.generate(cfg, np.arange(0, 1_000_000, 50))
+    qs = [N.Query(p.to_ir()) for p in W.multi_queries(64)]
+    s = N.Session(qs)
+    s.push(off, cols)
+    total = 0
+    for i, q in enumerate(qs):
+        r = oracle.run(q.ir, off, cols, threads=16)
+        emit = r["emit_pos"].astype(np.uint64) - off[r["key"].astype(np.int64)]
+        pk = np.repeat(r["key"].astype(np.int64), np.diff(r["pair_off"].astype(np.int64)))
+        pseq = r["pair_pos"].astype(np.uint64) - off[pk]
+        want = (r["n_matches"], W.match_digest(r["key"], emit, r["pair_off"], pseq, r["pair_stage"]),
+                int(np.count_nonzero(r["err_code"])))
+        assert s.digest(i) + (int(np.count_nonzero(s.key_errors(i)[0])),) == want, i
+        total += r["n_matches"]
+    assert total > 300_000
 
 
 @pytest.mark.parametrize("tier", TIERS)
