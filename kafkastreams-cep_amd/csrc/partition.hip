@@ -211,28 +211,46 @@ __global__ void __launch_bounds__(256) gather_cols_tr(const uint32_t* __restrict
   for (int k = 0; k < kTrKeys; k++) most = s_off[k + 1] - s_off[k] > most ? s_off[k + 1] - s_off[k] : most;
   const int nk_cols = nf + (ts_in ? 1 : 0);
   for (uint64_t c0 = 0; c0 < most; c0 += kTrChunk) {
-    // the chunk's permutation entries: wave w, keys 8w .. 8w+7, lane = event
+    // the chunk's permutation entries: wave w, keys 8w .. 8w+7, lane = event (every load in
+    // flight before the first LDS store: the scheduler would wait on each in turn)
+    uint32_t src[kTrKeys / 4];
 #pragma unroll
     for (int i = 0; i < kTrKeys / 4; i++) {
       const int k = w * (kTrKeys / 4) + i;
       const uint64_t j = c0 + (uint64_t)lane;
-      if (s_off[k] + j < s_off[k + 1]) s_src[k][lane] = perm[s_off[k] + j];
+      src[i] = s_off[k] + j < s_off[k + 1] ? perm[s_off[k] + j] : 0u;
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kTrKeys / 4; i++) s_src[w * (kTrKeys / 4) + i][lane] = src[i];
     __syncthreads();
     for (int f = 0; f < nk_cols; f++) {
       const bool is_ts = f == nf;
       const bool wide = is_ts || ((wide_mask >> f) & 1u);
-      // gather, key-minor: thread t reads key t mod 32, events t / 32 + 8 r
+      // gather, key-minor: thread t reads key t mod 32, events t / 32 + 8 r (all 8 loads in
+      // flight before the LDS stores)
+      uint64_t v[kTrChunk / 8];
+      const int k = tid % kTrKeys;
+      // (loads without a branch - a position past the key's events reads event 0 and is dropped -
+      // so they issue back to back: under a branch each waited for the one before)
+      uint32_t sj[kTrChunk / 8];
 #pragma unroll
       for (int r = 0; r < kTrChunk / 8; r++) {
-        const int k = tid % kTrKeys, j = tid / kTrKeys + 8 * r;
-        if (s_off[k] + c0 + (uint64_t)j < s_off[k + 1]) {
-          const uint32_t src = s_src[k][j];
-          s_val[k][j] = is_ts ? (uint64_t)ts_in[src]
-                              : wide ? (uint64_t)((const int64_t*)in.p[f])[src]
-                                     : (uint64_t)(uint32_t)((const int32_t*)in.p[f])[src];
-        }
+        const int j = tid / kTrKeys + 8 * r;
+        sj[r] = s_off[k] + c0 + (uint64_t)j < s_off[k + 1] ? s_src[k][j] : 0u;
       }
+      if (wide) {  // (block-uniform)
+        const int64_t* col = is_ts ? ts_in : (const int64_t*)in.p[f];
+#pragma unroll
+        for (int r = 0; r < kTrChunk / 8; r++) v[r] = (uint64_t)col[sj[r]];
+      } else {
+        const uint32_t* col = (const uint32_t*)in.p[f];
+#pragma unroll
+        for (int r = 0; r < kTrChunk / 8; r++) v[r] = col[sj[r]];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < kTrChunk / 8; r++) s_val[tid % kTrKeys][tid / kTrKeys + 8 * r] = v[r];
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < kTrKeys / 4; i++) {
