@@ -39,6 +39,7 @@ namespace cep {
 
 constexpr int kIngestBlock = 256;
 constexpr uint32_t kIngestLds = 16384;  // bytes of record text staged per block (avg record <= 64 B)
+static_assert(kIngestLds % (16 * kIngestBlock) == 0, "the staging loads: whole 16-B chunks per thread");
 constexpr int32_t kPending = -1;          // pass 1 left the record to the general state machine
 
 template <typename T>
@@ -73,7 +74,21 @@ __global__ void __launch_bounds__(kIngestBlock) decode_stock_json_kernel(
   const bool staged = (g1 - g0) * 16 <= kIngestLds;
   if (staged) {
     const uint4* src = (const uint4*)((uintptr_t)bytes - skew);
-    for (uint64_t c = g0 + threadIdx.x; c < g1; c += kIngestBlock) tile[c - g0] = src[c];
+    // every chunk load of the thread in flight before its LDS stores (a load-store loop waited
+    // for each load in turn)
+    constexpr int kIt = kIngestLds / 16 / kIngestBlock;
+    uint4 v[kIt];
+#pragma unroll
+    for (int i = 0; i < kIt; i++) {
+      const uint64_t c = g0 + threadIdx.x + (uint64_t)i * kIngestBlock;
+      v[i] = c < g1 ? src[c] : uint4{0u, 0u, 0u, 0u};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kIt; i++) {
+      const uint64_t c = g0 + threadIdx.x + (uint64_t)i * kIngestBlock;
+      if (c < g1) tile[c - g0] = v[i];
+    }
     __syncthreads();
   }
   const uint64_t r = r0 + threadIdx.x;
