@@ -9,6 +9,7 @@ one warmup push and prints one JSON line per mode on stdout.
     python profiles/workload.py cfg5 [--keys 125000]    64 stock-query variants, one batch
     python profiles/workload.py stream [--slices 10]    cfg 3 as consecutive streaming batches
     python profiles/workload.py shards [--world 8]      each rank's shard of cfg 3 alone
+    python profiles/workload.py arrival                 cfg 3 in arrival order (partition + NFA)
 
 $CEP_PROF=1 (set before the query is compiled) makes libcep print the kernel's time split
 (nfa_lane.h CEP_PROF) on stderr per launch.
@@ -63,6 +64,20 @@ def main():
         res["runs"] = timed(s, stream, args.steps)
         tot = [bench.match_figures(s, i, stream.n_keys) for i in range(64)]
         res.update(matches=sum(t[0] for t in tot), pairs=sum(t[1] for t in tot), key_errors=sum(t[2] for t in tot))
+        print(json.dumps(res), flush=True)
+        return
+    if m == "arrival":  # the end-to-end figure's push: partition on the GPU, then the NFA
+        st = N.synth_arrival_stream("stock", cfg.seed, args.keys, cfg.mean_events, 0, 0)
+        s = N.Session(N.Query(W.stock_query("readme").to_ir()))
+        s.push_arrival_device(st)
+        runs = []
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            s.push_arrival_device(st)
+            N.lib().cep_sync(s.h)
+            runs.append({"wall_ms": 1e3 * (time.perf_counter() - t0), "partition_ms": bench._partition_ms(s),
+                         "kernel_ms": s.stats(0)["kernel_ms"]})
+        res.update(events=st.n_events, runs=runs, checksum=f"{s.digest(0)[1]:016x}")
         print(json.dumps(res), flush=True)
         return
     stream = N.synth_stream("stock", cfg.seed, args.keys, cfg.mean_events)
