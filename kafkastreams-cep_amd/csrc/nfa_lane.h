@@ -82,9 +82,14 @@
 // Work counters for the CPU lane build (tests/lane_cpu, CEP_LANE_STATS); nothing on the GPU.
 #ifdef CEP_LANE_STATS
 extern uint64_t cep_lane_stats[10];  // events, records, walks, walk nodes, pred scans, flushes, chain steps, flush iters, exact conflicts, twin writes saved
+// every walk node (job key, the walk's event, the node, walk flags, the walker's version on
+// arrival): which extraction hops retrace a branch walk of the same event (tests/lane_cpu)
+void cep_lane_hop(uint32_t key, uint32_t t, uint32_t node, uint32_t flags, const cep::Dewey& w);
+#define CEP_HOP(k, t, s, f, w) cep_lane_hop(k, t, s, f, w)
 #define CEP_STAT(i) (cep_lane_stats[i]++)
 #else
 #define CEP_STAT(i) ((void)0)
+#define CEP_HOP(k, t, s, f, w) ((void)0)
 #endif
 
 // Time split of a launch (measurement builds only: $CEP_PROF at query compile, NfaArgs.prof):
@@ -124,11 +129,29 @@ constexpr uint32_t kPending = 0xFFFFFFFEu;  // ev_first of a record created at t
 #ifndef CEP_WALK_COMPAT2
 #define CEP_WALK_COMPAT2 0
 #endif
+// Fused branch + extraction walks (deferred walks).  A TAKE+PROCEED branch at a stage followed by
+// the final it forwards (NFA.java:231-246, then :111-115) queues a branch walk W_b from (stage,
+// event) and, in the finals pass of the same event, the final's extraction W_e from its new node
+// N_f, whose pointer leads back to W_b's start with W_b's version: from there both walk the same
+// path (a walk's choice of predecessor reads pointer versions and removed flags, which a branch
+// walk never changes and an extraction changes only behind itself), W_b adding 1 to every
+// node's refs and W_e taking 1 off.  When W_e directly follows W_b in the lane's queue (no walk
+// between them could observe W_b's counts), W_b is skipped and W_e, from W_b's start node on,
+// leaves refs as they are - deleting a node and removing its pointer exactly when the sequence
+// would (refs 0 before W_b).  W_e's first hop touches N_f alone, which W_b never reads, so it
+// commutes with W_b.  A failure W_b would meet (a dead node) W_e meets at the same node and
+// event; the key stops there either way and its unwound buffer is never read.  Measured on the
+// CPU lane build (profiles/r06/hops): 96-97 % of extraction hops retrace a branch walk of the
+// same event, half of all walk hops (config 3's README query and config 5's 64 queries).
+#ifndef CEP_WALK_FUSE
+#define CEP_WALK_FUSE CEP_WALK_COMPAT2
+#endif
 constexpr uint32_t kQuietChunk = CEP_QUIET_CHUNK;  // events a runs-free lane scans per driver step
 constexpr int kJobDrain = CEP_JOB_DRAIN;  // lanes at a job's end that make the wave drain its walks
 constexpr uint32_t kWalkFlush = CEP_WALK_FLUSH;    // a queue this long drains the wave's walk queues
 constexpr int kWalkQuads = 2 + (kLayoutPairs + 1) / 2;  // {sk|flags|n, ev, first, len} pairs {t}
 constexpr uint32_t kWalkEmit = 1, kWalkBranch = 2;
+constexpr uint32_t kWalkFused = 16;  // (runtime only) an extraction past the start of the branch walk it absorbed
 // the entry's `first` field holds the walk's start node itself (the record's node hint, live
 // when the walk was queued - an epsilon record's hint is its node of (stage key, event)): no
 // lookup at the walk's start.  Exact: no node is taken from the pool during a flush, so a
@@ -867,6 +890,7 @@ struct Lane {
       return false;
     }
     CEP_STAT(3);
+    CEP_HOP(key, t, s, flags, w);
     CEP_PACC(11, 1);
     Node& n = A.nodes[s];
     WalkPre P;
@@ -884,7 +908,8 @@ struct Lane {
     if (flags & kWalkBranch) {
       nrefs = refs + 1;
     } else {
-      left = refs == 0 ? 0 : refs - 1;
+      // (fused: the skipped branch walk's +1 and this walk's -1 - refs stays, left = refs)
+      left = (flags & kWalkFused) ? refs : refs == 0 ? 0 : refs - 1;
       nrefs = left;
       if (left == 0 && (meta >> 16) <= 1) {  // store.delete
         if (A.defer && lk > wid) {  // a put made after this walk was queued found the node live:
@@ -1020,6 +1045,9 @@ struct Lane {
     Dewey w;
     dw_init(w, 0);
     bool active = false, draining = part;
+#if CEP_WALK_FUSE
+    uint32_t fuse_at = CEP_NONE;  // the absorbed branch walk's start node (the fused mode from there)
+#endif
     uint32_t cut = CEP_NONE;   // put-log entry of the first put a walk's delete makes throw
     uint32_t conf = CEP_NONE;  // the node of this step's conflicting delete
 #if CEP_PARTIAL_DRAIN == 1
@@ -1068,13 +1096,64 @@ struct Lane {
         w = dw_pin(w);
         t = reinterpret_cast<const uint32_t*>(WQ(qs, kWalkQuads - 1))[0];
         i++;
-        if (!walk_start(flags, h.x & 0xFF, h.y, h.z, t, s, npa, np)) {
+        v4u hs = h;
+#if CEP_WALK_FUSE
+        fuse_at = CEP_NONE;
+        // a branch walk directly followed by an extraction of the same event that retraces it
+        // (CEP_WALK_FUSE above): skip it, the extraction absorbs it from its start node on
+        if ((flags & kWalkBranch) && i < wq_n && (cut == CEP_NONE || id0 + i < PL(cut)->y)) {
+          const uint32_t qe = wq_slot(i);
+          const v4u he = *WQ(qe, 0);
+          const uint32_t fe = (he.x >> 8) & 0xFF;
+          if ((fe & (kWalkEmit | kWalkBranch | kWalkHint)) == (kWalkEmit | kWalkHint) &&
+              reinterpret_cast<const uint32_t*>(WQ(qe, kWalkQuads - 1))[0] == t) {
+            const uint32_t sb = (flags & kWalkHint) ? h.z : lookup(h.x & 0xFF, h.z);
+            Dewey we;
+            we.n = he.x >> 24;
+            we.len = he.w;
+#pragma unroll
+            for (int k = 0; k < (kDeweyPairs + 1) / 2; k++) {
+              v4u d = {0, 0, 0, 0};
+              if (k == 0 || (uint32_t)(2 * k) < we.n) d = *WQ(qe, 1 + k);
+              we.v[2 * k] = (int32_t)d.x;
+              we.c[2 * k] = d.y;
+              if (2 * k + 1 < kDeweyPairs) {
+                we.v[2 * k + 1] = (int32_t)d.z;
+                we.c[2 * k + 1] = d.w;
+              }
+            }
+            we = dw_pin(we);
+            const uint32_t nf = he.z;  // N_f (the final record's node hint)
+            const v4u f0 = *NQ(nf, 0), f1 = *NQ(nf, 1);
+            if (sb != CEP_NONE && (f1.y & 0x100)) {
+              uint32_t nx = CEP_NONE;
+              Dewey nv;
+              bool same = false;
+              const uint32_t p = first_compat(f0.z, we, nx, nv, CEP_NONE, v4u{0, 0, 0, 0}, v4u{0, 0, 0, 0}, &same);
+              if (p != CEP_NONE && nx == sb && dw_equal(same ? we : nv, w)) {
+                fuse_at = sb;
+                flags = fe;
+                w = we;
+                hs = he;
+                i++;
+              }
+            }
+          }
+        }
+#endif
+        if (!walk_start(flags, hs.x & 0xFF, hs.y, hs.z, t, s, npa, np)) {
           draining = false;
           continue;
         }
         active = true;
       }
       CEP_STAT(7);
+#if CEP_WALK_FUSE
+      if (s == fuse_at && s != CEP_NONE) {
+        flags |= kWalkFused;
+        fuse_at = CEP_NONE;
+      }
+#endif
       const bool more = walk_node(flags, s, w, t, id0 + i - 1, np, conf);
       if (conf != CEP_NONE) {
         const uint32_t k = first_put_after(conf, id0 + i - 1);

@@ -123,6 +123,9 @@ def run(ir, key_off, cols, rcap=32, defer=True, streaming=False, reset=True, bit
     lib.lane_stats(st)
     m["stats"] = dict(zip(("events", "records", "walks", "walk_nodes", "pred_scans", "flushes", "chain_steps",
                            "flush_iters", "exact_conflicts", "twin_writes_saved"), list(st)))
+    hops = (C.c_uint64 * 4)()
+    lib.lane_hop_stats(hops)
+    m["stats"].update(zip(("hops_branch", "hops_emit", "hops_emit_retrace", "hops_remove"), list(hops)))
     if _group:
         return m
     m["emit_pos"] = (key_off[key.astype(np.int64)] + emit).astype(np.uint64)

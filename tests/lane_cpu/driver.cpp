@@ -9,6 +9,8 @@
 #include <cstdint>
 #include <algorithm>
 #include <cstdlib>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include QUERY_SRC
@@ -19,6 +21,43 @@ thread_local LaneDim3 blockIdx, threadIdx, blockDim, gridDim;
 static void wave_body(void* a) { cep_nfa_jit(*static_cast<cep::NfaArgs*>(a)); }
 uint64_t cep_lane_stats[10];
 extern "C" void lane_stats(uint64_t* out) { std::memcpy(out, cep_lane_stats, sizeof cep_lane_stats); }
+
+// Walk hops by kind (nfa_lane.h CEP_HOP): branch, extraction (emit), extraction hops at a node
+// a branch walk of the same key and event passed with the same walker version (the hops a
+// fused branch + extraction walk would not repeat), remove-only.  Walks drain in queue order,
+// so a key's walk events only grow: the key keeps the (node, version) set of its latest event.
+namespace {
+struct HopSet {
+  uint32_t t = 0xFFFFFFFFu;
+  std::unordered_set<uint64_t> seen;
+};
+std::unordered_map<uint32_t, HopSet> g_hop_keys;
+uint64_t g_hops[4];
+uint64_t ver_hash(const cep::Dewey& w) {
+  uint64_t h = 1469598103934665603ull ^ w.len;
+  for (uint32_t i = 0; i < w.n && i < (uint32_t)cep::kDeweyPairs; i++)
+    h = (h ^ ((uint64_t)(uint32_t)w.v[i] << 32 | w.c[i])) * 1099511628211ull;
+  return h;
+}
+}  // namespace
+void cep_lane_hop(uint32_t key, uint32_t t, uint32_t node, uint32_t flags, const cep::Dewey& w) {
+  HopSet& hs = g_hop_keys[key];
+  if (hs.t != t) {
+    hs.t = t;
+    hs.seen.clear();
+  }
+  const uint64_t id = ((uint64_t)node << 32) ^ (ver_hash(w) & 0xFFFFFFFFull);
+  if (flags & cep::kWalkBranch) {
+    g_hops[0]++;
+    hs.seen.insert(id);
+  } else if (flags & cep::kWalkEmit) {
+    g_hops[1]++;
+    if (hs.seen.count(id)) g_hops[2]++;
+  } else {
+    g_hops[3]++;
+  }
+}
+extern "C" void lane_hop_stats(uint64_t* out) { std::memcpy(out, g_hops, sizeof g_hops); }
 
 namespace {
 std::vector<uint32_t> g_key, g_emit, g_seq;
@@ -88,6 +127,8 @@ extern "C" int lane_run(uint64_t nk, const uint64_t* key_off, const void* const*
   using namespace cep;
   signal(SIGSEGV, on_fault);
   std::memset(cep_lane_stats, 0, sizeof cep_lane_stats);
+  std::memset(g_hops, 0, sizeof g_hops);
+  g_hop_keys.clear();
   const uint64_t ne = key_off[nk];
   std::vector<Node> nodes_batch, *nodes_p = &nodes_batch;
   std::vector<Pred> preds_batch, *preds_p = &preds_batch, preds0_batch, *preds0_p = &preds0_batch;

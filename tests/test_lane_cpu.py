@@ -472,3 +472,34 @@ def _run_source(ir, source, off, cols):
     pk = np.repeat(m["key"].astype(np.int64) % (len(key_off) - 1), np.diff(m["pair_off"].astype(np.int64)))
     m["pair_pos"] = (key_off[pk] + m["pair_seq"]).astype(np.uint64)
     return m
+
+
+@pytest.mark.parametrize("case", ["readme", "cfg4s", "kats"] + [f"fuzz{s}" for s in range(24)])
+def test_lane_fused_walks(case, monkeypatch):
+    """Fused branch + extraction walks (nfa_lane.h CEP_WALK_FUSE: on in kernel groups, forced
+    on here for single queries) give the oracle's matches and errors; on the stock streams the
+    fused build walks fewer branch hops than the unfused one (the walk-hop counters of the CPU
+    lane build) with every extraction hop still walked."""
+    if case in ("readme", "cfg4s"):
+        off, cols = W.generate(W.CONFIGS[3], np.arange(0, 1_000_000, 7919))
+        q = W.stock_query("readme") if case == "readme" else W.any_kleene_query(carry_volume=True)
+        cases = [(q.to_ir(), off, cols)]
+    elif case == "kats":
+        cases = []
+        for n in KAT_CASES:
+            q, off, cols = build_case(n, kats()[n])
+            cases.append((q.to_ir(), off, cols))
+    else:
+        seed = int(case[4:])
+        off, cols = random_stream(seed, 60, 14)
+        cases = [(random_query(seed).to_ir(), off, cols)]
+    for ir, off, cols in cases:
+        monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_WALK_FUSE=0")
+        plain = lane_cpu.run(ir, off, cols)
+        monkeypatch.setenv("CEP_LANE_DEFINES", "CEP_WALK_FUSE=1")
+        fused = lane_cpu.run(ir, off, cols)
+        lane_cpu.assert_same(fused, oracle.run(ir, off, cols), off)
+        assert fused["stats"]["hops_emit"] == plain["stats"]["hops_emit"]
+        assert fused["stats"]["hops_branch"] <= plain["stats"]["hops_branch"]
+        if case == "readme":
+            assert fused["stats"]["hops_branch"] < plain["stats"]["hops_branch"]
